@@ -1,0 +1,163 @@
+/*
+ * vit_hip.h — C-ABI of libvit_hip.so, the MI355X (gfx950 / CDNA4) compute library behind the drop-in
+ * `VisionTransformer` package (vision-transformer_amd/VisionTransformer).
+ *
+ * The reference (SiddhantSKarki/Vision-Transformer) has no FFI: its boundary is the torch.nn.Module API and every op
+ * below replaces an ATen call site on the training hot path (SURVEY.md §2 table "ATen op call sites").  Each entry
+ * point cites the reference line(s) whose arithmetic it replaces.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + int64 sizes; no torch types; dtype enums below;
+ *   - `stream` is a hipStream_t passed as void*; every launch is asynchronous on it; no device sync, no allocation
+ *     (callers own all buffers and workspaces — the PyTorch caching allocator in the host package);
+ *   - return 0 on success, a nonzero vit_status on failure with a thread-local message in vit_last_error();
+ *   - re-entrant; no global mutable state.
+ */
+#ifndef VIT_HIP_H
+#define VIT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VIT_ABI_VERSION 1
+
+typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
+typedef enum { VIT_F32 = 0, VIT_BF16 = 1 } vit_dtype;
+typedef enum { VIT_ACT_NONE = 0, VIT_ACT_RELU = 1, VIT_ACT_GELU = 2 } vit_act;
+
+int vit_abi_version(void);
+const char* vit_last_error(void);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * GEMM with fused epilogue:  C[i][j] = epi( alpha * sum_r A(i,r) * B(j,r) )
+ *   A(i,r) at a[i*lda + r] when a_kcontig, else a[r*lda + i]   (same for B with ldb / b_kcontig)
+ *   epi(v): v += beta*C_old (f32 out only); v += bias[j]; act; v *= (aux(i,j) > 0) when aux;
+ *           dropout(p, seed, index i*n + j) with 1/(1-p) scale; v += res(row(i), j) where row(i) = i % res_rowmod
+ *           (res_rowmod == 0: i); stored at C[orow(i)*ldc + j], orow(i) = (i/G)*Gs + i%G when out_group_rows = G > 0.
+ * Replaces: nn.Linear (transformer.py:12-18,38,56,58; vit.py:70,73), the conv-as-GEMM (vit.py:21-28), and all their
+ * autograd dgrad/wgrad GEMMs; dropout (transformer.py:47,59); residual adds (transformer.py:77-78); ReLU (:57).
+ * bf16 inputs run on v_mfma_f32_16x16x32_bf16 (fp32 accumulate); f32 inputs on v_mfma_f32_32x32x2_f32 (exact fp32).
+ * ------------------------------------------------------------------------------------------------------------ */
+typedef struct vit_gemm_desc {
+  const void* a;
+  const void* b;
+  void* c;
+  int64_t lda, ldb, ldc;
+  int64_t m, n, k;
+  int32_t a_kcontig, b_kcontig;
+  int32_t in_dtype;   /* vit_dtype of A and B */
+  int32_t out_dtype;  /* vit_dtype of C */
+  float alpha, beta;
+  const float* bias;  /* [n] or NULL */
+  int32_t act;        /* vit_act */
+  int32_t aux_dtype;
+  const void* aux;    /* relu-backward mask source (keep where aux > 0) or NULL */
+  int64_t ldaux;
+  const void* res;    /* residual added last, or NULL */
+  int64_t ldres;
+  int64_t res_rowmod;
+  int32_t res_dtype;
+  float dropout_p;    /* 0 disables */
+  uint32_t dropout_seed;
+  int32_t split_k;    /* >1: K split over workgroups, fp32 slabs in workspace, deterministic reduce */
+  int64_t out_group_rows, out_group_stride;
+  void* workspace;
+  int64_t workspace_bytes;
+} vit_gemm_desc;
+
+int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d);
+int vit_gemm(const vit_gemm_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * Patch embedding (vit.py:21-29,39-42).
+ *   vit_im2col: x[B][C][H][W] (x_dtype) -> cols[B*N][C*P*P] (dtype), column order (c, kh, kw) = conv weight order,
+ *               patch order row-major over (H/P, W/P).  The GEMM epilogue then adds conv bias + pos (res_rowmod = N)
+ *               and writes rows (b, n) to x0[b*T + n] (out_group_rows = N, out_group_stride = T).
+ *   vit_embed_cls: x0[b*T + N][:] = cls[b][:] + pos[N][:]   (CLS appended LAST, vit.py:41)
+ * ------------------------------------------------------------------------------------------------------------ */
+int vit_im2col(const void* x, int32_t x_dtype, void* cols, int32_t dtype, int64_t B, int64_t C, int64_t H,
+               int64_t W, int64_t P, void* stream);
+int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, int64_t B, int64_t T, int64_t D,
+                  void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * LayerNorm (nn.LayerNorm, transformer.py:71-72,77-78; vit.py:72), fp32 statistics.
+ *   fwd: y = (x - mean) * rstd * gamma + beta; saves mean/rstd [rows].
+ *   bwd: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
+ *        dx_out = dx (+ dres when dres != NULL)                    — fused residual-gradient add (transformer.py:77-78)
+ *        drop_out = dx_out * keep(drop_seed, i*cols + j) / (1-p)    — fused dropout backward of the producer branch
+ *        dgamma/dbeta: per-workgroup partials in `partial` [2][nparts][cols], reduced by vit_colsum (deterministic).
+ * ------------------------------------------------------------------------------------------------------------ */
+int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma, const float* beta, void* y, int64_t ldy,
+                      float* mean, float* rstd, int64_t rows, int64_t cols, float eps, int32_t dtype, void* stream);
+int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols);
+int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
+                      const float* mean, const float* rstd, const void* dres, void* dx_out, void* drop_out,
+                      float drop_p, uint32_t drop_seed, float* partial, int64_t rows, int64_t cols, int32_t dtype,
+                      void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * Multi-head self-attention (transformer.py:9-31 per head, :44-45 concat): qkv[B*T][3*D] with Q at columns
+ * h*hd, K at D + h*hd, V at 2D + h*hd; o[B*T][D] (heads concatenated, same column order as torch.cat).
+ *   o = softmax(scale * Q K^T) V with scale = sqrt(hd) in the reference (multiplied, transformer.py:24);
+ *   lse[B][H][T] (natural log of the row softmax denominator, scaled-logit domain) saved for backward;
+ *   probs [B][H][T][T] f32 optional (the `.attention_probs` side attribute, transformer.py:48).
+ * bf16 & hd == 64: flash-style MFMA kernels (K/V tiles in LDS, online softmax); otherwise a generic VALU kernel.
+ * bwd: dqkv[B*T][3*D]; workspace = vit_attn_bwd_workspace_bytes.
+ * ------------------------------------------------------------------------------------------------------------ */
+int vit_attn_fwd(const void* qkv, void* o, float* lse, float* probs, int64_t B, int64_t T, int64_t H, int64_t hd,
+                 float scale, int32_t dtype, void* stream);
+int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
+int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, const float* lse, void* dqkv, int64_t B,
+                 int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * Reductions / elementwise.
+ *   vit_colsum: out[j] = beta*out[j] + sum_i x[i*ldx + j]  (bias / pos / LN-affine gradients); deterministic.
+ *   vit_copy2d: dst[orow(i)*ldd + j] = beta*dst + src[irow(i)*lds + j] with optional row grouping on the source
+ *               (irow(i) = (i/G)*Gs + i%G) — token-0 gather (vit.py:80), CLS-gradient copy, dropout-free casts.
+ *   vit_dropout_bwd: y = x * keep(seed, i) / (1-p)  (transformer.py:47,59 backward).
+ *   vit_gelu_fwd/bwd: exact-erf GELU (vit.py:71) on f32.
+ *   vit_softmax_xent: per-row softmax cross entropy (train.py:81,93): loss = mean_i(-log p[i][y_i]) and
+ *                     dlogits = (softmax - onehot) / rows, in one pass.
+ * ------------------------------------------------------------------------------------------------------------ */
+int64_t vit_colsum_workspace_bytes(int64_t rows, int64_t cols);
+int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t cols, float* out, float beta,
+               void* workspace, void* stream);
+int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,
+               int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
+               void* stream);
+int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed, void* stream);
+int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream);
+int vit_gelu_bwd(const float* x, const float* dy, float* dx, int64_t n, void* stream);
+int vit_softmax_xent(const float* logits, const int64_t* labels, int64_t rows, int64_t classes, float* loss,
+                     float* dlogits, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * Optimizer (train.py:66,96: torch.optim.AdamW(lr, weight_decay=1e-4), betas (0.9, 0.999), eps 1e-8) as ONE
+ * multi-tensor launch over a device-resident chunk table; also refreshes the compute-dtype shadow weights.
+ *   p *= 1 - lr*wd;  m = b1*m + (1-b1)*g*gs;  v = b2*v + (1-b2)*(g*gs)^2;
+ *   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps);  shadow = (dtype) p   (gs = grad_scale, e.g. 1/world_size)
+ * vit_pack: shadow = (dtype) src over the same table layout (used after external writes to the fp32 params).
+ * ------------------------------------------------------------------------------------------------------------ */
+typedef struct vit_tensor_chunk {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  void* shadow; /* NULL: no shadow for this chunk */
+  int64_t n;
+} vit_tensor_chunk;
+
+int vit_adamw(const vit_tensor_chunk* table_dev, int64_t nchunks, float lr, float beta1, float beta2, float eps,
+              float weight_decay, float bias_corr1, float bias_corr2, float grad_scale, int32_t shadow_dtype,
+              void* stream);
+int vit_pack(const vit_tensor_chunk* table_dev, int64_t nchunks, int32_t shadow_dtype, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIT_HIP_H */

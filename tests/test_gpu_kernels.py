@@ -1,0 +1,262 @@
+"""Per-kernel numerics on the MI355X: each HIP kernel (called through the C-ABI) against a plain torch fp32/fp64
+reference of the same op.  Integer-valued operands make the MFMA layout checks exact (asymmetric data, so a
+transposed fragment or C-write cannot pass)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from VisionTransformer import _ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def _ints(shape, lo=-4, hi=5, gen=None, dtype=torch.bfloat16):
+    return torch.randint(lo, hi, shape, generator=gen).to(dtype).to(DEV)
+
+
+def _ref_op(A, B, akc, bkc):
+    """C[i][j] = sum_r A(i,r) B(j,r) in float64 from the stored layouts."""
+    Ai = A.double() if akc else A.double().t()
+    Bj = B.double() if bkc else B.double().t()
+    return Ai @ Bj.t()
+
+
+LAYOUTS = [(True, True), (True, False), (False, False)]
+
+
+@pytest.mark.parametrize("akc,bkc", LAYOUTS)
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (200, 136, 72), (56, 40, 24), (136, 8, 2000)])
+def test_gemm_bf16_exact_integers(akc, bkc, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = _ints((M, K) if akc else (K, M), gen=g)
+    B = _ints((N, K) if bkc else (K, N), gen=g)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    _ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), N, a_kcontig=akc, b_kcontig=bkc)
+    ref = _ref_op(A, B, akc, bkc)
+    assert torch.equal(C.double(), ref), (C.double() - ref).abs().max()
+
+
+def test_gemm_bf16_rejects_unaligned_contiguous_dim():
+    A = torch.zeros(24, 50, dtype=torch.bfloat16, device=DEV)   # rowstrided A with M = 50 (not a multiple of 8)
+    B = torch.zeros(24, 40, dtype=torch.bfloat16, device=DEV)
+    C = torch.empty(50, 40, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 8"):
+        _ops.gemm(A, B, C, 50, 40, 24, 50, 40, 40, a_kcontig=False, b_kcontig=False)
+
+
+@pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(64, 64, 16), (100, 70, 33), (257, 130, 300), (10, 1000, 3072)])
+def test_gemm_f32(akc, bkc, M, N, K):
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn((M, K) if akc else (K, M), generator=g).to(DEV)
+    B = torch.randn((N, K) if bkc else (K, N), generator=g).to(DEV)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    _ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), N, a_kcontig=akc, b_kcontig=bkc)
+    ref = _ref_op(A, B, akc, bkc)
+    tol = 2e-6 * math.sqrt(K) * ref.abs().max().item()
+    assert (C.double() - ref).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue_bias_relu_dropout_residual(dtype):
+    torch.manual_seed(0)
+    M, N, K = 394, 256, 128
+    x = torch.randn(M, K, device=DEV).to(dtype)
+    w = (torch.randn(N, K, device=DEV) * 0.1).to(dtype)
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).to(dtype)
+    out = torch.empty(M, N, dtype=dtype, device=DEV)
+    seed, p = 1234, 0.2
+    _ops.gemm(x, w, out, M, N, K, K, K, N, bias=bias, res=res, ldres=N, dropout_p=p, seed=seed)
+    import numpy as np
+    from oracle.vit_oracle import dropout_keep
+    keep = dropout_keep(seed, (M, N), p).to(DEV)
+    y = x.float() @ w.float().t() + bias
+    ref = res.float() + y * keep * (1 / (1 - p))
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert (out.float() - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item())
+    # relu + aux mask variants
+    out2 = torch.empty(M, N, dtype=dtype, device=DEV)
+    _ops.gemm(x, w, out2, M, N, K, K, K, N, bias=bias, act=_ops.ACT_RELU)
+    ref2 = torch.relu(y)
+    assert (out2.float() - ref2).abs().max().item() <= tol * max(1.0, ref2.abs().max().item())
+    out3 = torch.empty(M, N, dtype=dtype, device=DEV)
+    _ops.gemm(x, w, out3, M, N, K, K, K, N, aux=res, ldaux=N)
+    ref3 = (x.float() @ w.float().t()) * (res.float() > 0)
+    assert (out3.float() - ref3).abs().max().item() <= tol * max(1.0, ref3.abs().max().item())
+
+
+def test_gemm_row_group_and_rowmod():
+    """patch-embed epilogue: rows (b, n) -> b*T + n, + pos[n] (res_rowmod = N)"""
+    torch.manual_seed(1)
+    B, N, T, D, K = 3, 196, 197, 256, 768
+    cols = torch.randn(B * N, K, device=DEV).bfloat16()
+    w = (torch.randn(D, K, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(D, device=DEV)
+    pos = torch.randn(T, D, device=DEV)
+    x0 = torch.full((B * T, D), 7.0, device=DEV).bfloat16()
+    _ops.gemm(cols, w, x0, B * N, D, K, K, K, D, bias=bias, res=pos, ldres=D, res_rowmod=N, out_group=(N, T))
+    ref = (cols.float() @ w.float().t() + bias).view(B, N, D) + pos[:N]
+    got = x0.view(B, T, D)
+    assert (got[:, :N].float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    assert torch.all(got[:, N] == 7.0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_split_k_wgrad(dtype):
+    torch.manual_seed(2)
+    M, N, K = 5000, 256, 192          # wgrad form: dW[N][K] = dY^T X with reduction over M rows
+    dy = torch.randn(M, N, device=DEV).to(dtype)
+    x = torch.randn(M, K, device=DEV).to(dtype)
+    dw = torch.randn(N, K, device=DEV)
+    dw0 = dw.clone()
+    _ops.gemm(dy, x, dw, N, K, M, N, K, K, a_kcontig=False, b_kcontig=False, beta=1.0, split_k=7)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    tol = (1e-5 if dtype == torch.float32 else 1e-5) * ref.abs().max().item() * 10
+    assert (dw.double() - ref).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [64, 192, 768, 3072])
+def test_layernorm_fwd_bwd(dtype, cols):
+    torch.manual_seed(3)
+    rows = 300
+    x = (torch.randn(rows, cols, device=DEV) * 2 + 0.5).to(dtype)
+    g = torch.rand(cols, device=DEV) + 0.5
+    b = torch.randn(cols, device=DEV)
+    y, mean, rstd = _ops.layernorm_fwd(x, g, b)
+    xr = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (cols,), gr, br, 1e-5)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert (y.float() - yr).abs().max().item() <= tol * 4
+    dy = torch.randn(rows, cols, device=DEV).to(dtype)
+    dres = torch.randn(rows, cols, device=DEV).to(dtype)
+    yr.backward(dy.float())
+    dx = torch.empty_like(x)
+    drop = torch.empty_like(x)
+    part = _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, drop_out=drop, drop_p=0.2, drop_seed=99)
+    dg = torch.empty(cols, device=DEV)
+    db = torch.empty(cols, device=DEV)
+    _ops.colsum(part[0], part.shape[1], cols, cols, dg)
+    _ops.colsum(part[1], part.shape[1], cols, cols, db)
+    ref_dx = xr.grad + dres.float()
+    scale = ref_dx.abs().max().item()
+    assert (dx.float() - ref_dx).abs().max().item() <= tol * 4 * scale
+    assert (dg - gr.grad).abs().max().item() <= tol * 4 * gr.grad.abs().max().item()
+    assert (db - br.grad).abs().max().item() <= tol * 4 * br.grad.abs().max().item()
+    from oracle.vit_oracle import dropout_keep
+    keep = dropout_keep(99, (rows, cols)).to(DEV)
+    assert torch.equal(drop.float(), (dx.float() * keep * 1.25).to(dtype).float())
+
+
+def _attn_ref(qkv, B, T, H, hd, scale):
+    D = H * hd
+    q, k, v = qkv.float().view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    p = torch.softmax(s, -1)
+    o = (p @ v).permute(0, 2, 1, 3).reshape(B * T, D)
+    lse = torch.logsumexp(s, -1)
+    return o, lse, p
+
+
+@pytest.mark.parametrize("dtype,hd", [(torch.float32, 16), (torch.float32, 64), (torch.bfloat16, 64),
+                                      (torch.bfloat16, 32)])
+@pytest.mark.parametrize("T", [5, 17, 197, 577])
+@pytest.mark.parametrize("amp", [0.15, 1.0])
+def test_attention_fwd_bwd(dtype, hd, T, amp):
+    torch.manual_seed(T + hd)
+    B, H = 2, 3
+    D = H * hd
+    scale = hd ** 0.5                     # the reference multiplies by sqrt(hd) (transformer.py:24)
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * amp).to(dtype)
+    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, scale)
+    x = qkv.float().requires_grad_(True)
+    o_ref, lse_ref, _ = _attn_ref(x, B, T, H, hd, scale)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert (o.float() - o_ref).abs().max().item() <= tol * max(1.0, o_ref.abs().max().item())
+    assert (lse - lse_ref).abs().max().item() <= 1e-3 * max(1.0, lse_ref.abs().max().item())
+    d_o = torch.randn(B * T, D, device=DEV).to(dtype)
+    dqkv = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale)
+    o_ref.backward(d_o.float())
+    g = x.grad
+    err = (dqkv.float() - g).abs().max().item()
+    assert err <= tol * 5 * max(1.0, g.abs().max().item()), err
+
+
+def test_attention_probs_generic():
+    torch.manual_seed(5)
+    B, T, H, hd = 2, 17, 2, 64
+    qkv = (torch.randn(B * T, 3 * H * hd, device=DEV) * 0.2)
+    probs = torch.empty(B, H, T, T, device=DEV)
+    _ops.attn_fwd(qkv, B, T, H, hd, hd ** 0.5, probs=probs)
+    _, _, p = _attn_ref(qkv, B, T, H, hd, hd ** 0.5)
+    assert (probs - p).abs().max().item() < 1e-5
+
+
+def test_misc_kernels():
+    torch.manual_seed(6)
+    # im2col (vit.py:21-29 conv as GEMM)
+    x = torch.randn(2, 3, 64, 48, device=DEV)
+    cols = _ops.im2col(x, 16, torch.float32)
+    ref = x.view(2, 3, 4, 16, 3, 16).permute(0, 2, 4, 1, 3, 5).reshape(2 * 12, 768)
+    assert torch.equal(cols, ref)
+    colsb = _ops.im2col(x, 16, torch.bfloat16)
+    assert torch.equal(colsb, ref.bfloat16())
+    # colsum
+    a = torch.randn(1000, 300, device=DEV)
+    out = torch.ones(300, device=DEV)
+    _ops.colsum(a, 1000, 300, 300, out, beta=1.0)
+    assert (out - (a.sum(0) + 1)).abs().max().item() < 1e-3
+    # copy2d with grouped source rows + accumulate
+    src = torch.randn(4 * 5, 8, device=DEV)
+    dst = torch.ones(4 * 3, 8, device=DEV)
+    _ops.copy2d(src, 8, dst, 8, 12, 8, group=(3, 5), beta=1.0)
+    assert torch.allclose(dst, src.view(4, 5, 8)[:, :3].reshape(12, 8) + 1)
+    # GELU
+    z = torch.randn(5000, device=DEV) * 3
+    assert (_ops.gelu_fwd(z) - torch.nn.functional.gelu(z)).abs().max().item() < 1e-5
+    zr = z.clone().requires_grad_(True)
+    torch.nn.functional.gelu(zr).backward(torch.ones_like(z))
+    assert (_ops.gelu_bwd(z, torch.ones_like(z)) - zr.grad).abs().max().item() < 1e-5
+    # softmax cross entropy (train.py:81,93)
+    lg = torch.randn(37, 1000, device=DEV) * 4
+    lb = torch.randint(0, 1000, (37,), device=DEV)
+    loss, dl = _ops.softmax_xent(lg, lb)
+    lr_ = lg.clone().requires_grad_(True)
+    lref = torch.nn.functional.cross_entropy(lr_, lb)
+    lref.backward()
+    assert abs(loss.item() - lref.item()) < 1e-5
+    assert (dl - lr_.grad).abs().max().item() < 1e-6
+    # dropout backward mask
+    from oracle.vit_oracle import dropout_keep
+    t = torch.randn(3000, device=DEV)
+    y = torch.empty_like(t)
+    _ops.dropout_bwd(t, y, 0.2, 4242)
+    keep = dropout_keep(4242, (3000,)).to(DEV)
+    assert torch.equal(y, t * keep * 1.25)
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(7)
+    shapes = [(300,), (70000,), (128, 64)]
+    ps = [torch.randn(s, device=DEV) for s in shapes]
+    gs = [torch.randn(s, device=DEV) for s in shapes]
+    ms = [torch.zeros_like(p) for p in ps]
+    vs = [torch.zeros_like(p) for p in ps]
+    sh = [torch.empty(s, dtype=torch.bfloat16, device=DEV) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-4)
+    table, n = _ops.build_chunk_table(list(zip(ps, gs, ms, vs, sh)), DEV)
+    for step in range(1, 4):
+        for r, g in zip(ref, gs):
+            r.grad = g.clone()
+        opt.step()
+        _ops.adamw(table, n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1 - 0.9 ** step, 1 - 0.999 ** step, 1.0, torch.bfloat16)
+    for p, r, s in zip(ps, ref, sh):
+        assert (p - r.detach()).abs().max().item() < 1e-6
+        assert torch.equal(s, p.bfloat16())

@@ -1,0 +1,219 @@
+"""Tensor-level wrappers over the C-ABI (no autograd here).  Every function launches on the current HIP stream
+(or `stream`) and returns immediately.  Shapes/dtypes are validated on the host; the kernels re-validate."""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32  # noqa: F401
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dtype_code(t):
+    try:
+        return _DT[t.dtype if isinstance(t, torch.Tensor) else t]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype if isinstance(t, torch.Tensor) else t}; use float32 or bfloat16")
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("VisionTransformer HIP path: tensors must live on a ROCm device (got CPU tensor); "
+                               "the CPU restatement under oracle/ is test infrastructure, not a fallback")
+
+
+def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=1.0, beta=0.0, bias=None,
+         act=ACT_NONE, aux=None, ldaux=0, res=None, ldres=0, res_rowmod=0, dropout_p=0.0, seed=0, split_k=1,
+         out_group=(0, 0), workspace=None, stream=None):
+    """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  Returns c."""
+    _need_cuda(a, b, c, bias, aux, res)
+    if a.dtype != b.dtype:
+        raise TypeError("gemm: A and B dtypes differ")
+    if bias is not None and bias.dtype != torch.float32:
+        raise TypeError("gemm: bias must be float32")
+    d = _lib.GemmDesc()
+    d.a, d.b, d.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
+    d.lda, d.ldb, d.ldc = lda, ldb, ldc
+    d.m, d.n, d.k = m, n, k
+    d.a_kcontig, d.b_kcontig = int(a_kcontig), int(b_kcontig)
+    d.in_dtype, d.out_dtype = dtype_code(a), dtype_code(c)
+    d.alpha, d.beta = alpha, beta
+    d.bias = None if bias is None else bias.data_ptr()
+    d.act = act
+    if aux is not None:
+        d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), ldaux, dtype_code(aux)
+    if res is not None:
+        d.res, d.ldres, d.res_rowmod, d.res_dtype = res.data_ptr(), ldres, res_rowmod, dtype_code(res)
+    d.dropout_p, d.dropout_seed = dropout_p, seed & 0xFFFFFFFF
+    d.split_k = split_k
+    d.out_group_rows, d.out_group_stride = out_group
+    if split_k > 1:
+        need = _lib.load().vit_gemm_workspace_bytes(ctypes.byref(d))
+        if workspace is None or workspace.numel() * workspace.element_size() < need:
+            workspace = torch.empty(need // 4 + 1, dtype=torch.float32, device=c.device)
+        d.workspace, d.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    _lib.check(_lib.load().vit_gemm(ctypes.byref(d), _stream(stream)), "vit_gemm")
+    return c
+
+
+def linear(x2d, w, bias=None, out_dtype=None, act=ACT_NONE, **kw):
+    """y = act(x @ w^T + bias) for row-major x [M,K], w [N,K]."""
+    M, K = x2d.shape
+    N = w.shape[0]
+    y = torch.empty(M, N, dtype=out_dtype or x2d.dtype, device=x2d.device)
+    return gemm(x2d, w, y, M, N, K, x2d.stride(0), w.stride(0), N, bias=bias, act=act, **kw)
+
+
+def im2col(x, P, dtype, stream=None):
+    _need_cuda(x)
+    B, C, H, W = x.shape
+    n = (H // P) * (W // P)
+    cols = torch.empty(B * n, C * P * P, dtype=dtype, device=x.device)
+    _lib.call("vit_im2col", _ptr(x), dtype_code(x), _ptr(cols), dtype_code(dtype), B, C, H, W, P, _stream(stream))
+    return cols
+
+
+def embed_cls(cls, pos, x0, B, T, D, stream=None):
+    _lib.call("vit_embed_cls", _ptr(cls), _ptr(pos), _ptr(x0), dtype_code(x0), B, T, D, _stream(stream))
+
+
+def layernorm_fwd(x2d, gamma, beta, y=None, eps=1e-5, stream=None):
+    _need_cuda(x2d, gamma, beta)
+    rows, cols = x2d.shape
+    y = torch.empty_like(x2d) if y is None else y
+    mean = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    _lib.call("vit_layernorm_fwd", _ptr(x2d), x2d.stride(0), _ptr(gamma), _ptr(beta), _ptr(y), y.stride(0),
+              _ptr(mean), _ptr(rstd), rows, cols, eps, dtype_code(x2d), _stream(stream))
+    return y, mean, rstd
+
+
+def layernorm_bwd_parts(rows, cols):
+    return _lib.load().vit_layernorm_bwd_parts(rows, cols)
+
+
+def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, drop_p=0.0, drop_seed=0,
+                  partial=None, stream=None):
+    """dx_out = LN_bwd(dy) (+ dres); drop_out = dropout_bwd(dx_out); returns partial [2, parts, cols] f32
+    (dgamma / dbeta per workgroup) — reduce with colsum."""
+    rows, cols = x.shape
+    parts = layernorm_bwd_parts(rows, cols)
+    if partial is None:
+        partial = torch.empty(2, parts, cols, dtype=torch.float32, device=x.device)
+    _lib.call("vit_layernorm_bwd", _ptr(dy), dy.stride(0), _ptr(x), x.stride(0), _ptr(gamma), _ptr(mean), _ptr(rstd),
+              _ptr(dres), _ptr(dx_out), _ptr(drop_out), drop_p, drop_seed & 0xFFFFFFFF, _ptr(partial), rows, cols,
+              dtype_code(x), _stream(stream))
+    return partial
+
+
+def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, stream=None):
+    _need_cuda(qkv)
+    D = H * hd
+    o = torch.empty(B * T, D, dtype=qkv.dtype, device=qkv.device) if o is None else o
+    lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device) if lse is None else lse
+    _lib.call("vit_attn_fwd", _ptr(qkv), _ptr(o), _ptr(lse), _ptr(probs), B, T, H, hd, scale, dtype_code(qkv),
+              _stream(stream))
+    return o, lse
+
+
+def attn_bwd_workspace_bytes(B, T, H, hd, dtype):
+    return _lib.load().vit_attn_bwd_workspace_bytes(B, T, H, hd, dtype_code(dtype))
+
+
+def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, stream=None):
+    dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
+    need = attn_bwd_workspace_bytes(B, T, H, hd, qkv.dtype)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(max(need // 4, 1), dtype=torch.float32, device=qkv.device)
+    _lib.call("vit_attn_bwd", _ptr(qkv), _ptr(o), _ptr(d_o), _ptr(lse), _ptr(dqkv), B, T, H, hd, scale,
+              dtype_code(qkv), _ptr(workspace), _stream(stream))
+    return dqkv
+
+
+def colsum(x, rows, cols, ldx, out, beta=0.0, workspace=None, stream=None):
+    need = _lib.load().vit_colsum_workspace_bytes(rows, cols)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
+    _lib.call("vit_colsum", _ptr(x), ldx, dtype_code(x), rows, cols, _ptr(out), beta, _ptr(workspace),
+              _stream(stream))
+    return out
+
+
+def copy2d(src, lds, dst, ldd, rows, cols, group=(0, 0), beta=0.0, stream=None):
+    _lib.call("vit_copy2d", _ptr(src), lds, dtype_code(src), _ptr(dst), ldd, dtype_code(dst), rows, cols, group[0],
+              group[1], beta, _stream(stream))
+    return dst
+
+
+def dropout_bwd(x, y, p, seed, stream=None):
+    _lib.call("vit_dropout_bwd", _ptr(x), _ptr(y), dtype_code(x), x.numel(), p, seed & 0xFFFFFFFF, _stream(stream))
+    return y
+
+
+def gelu_fwd(x, y=None, stream=None):
+    y = torch.empty_like(x) if y is None else y
+    _lib.call("vit_gelu_fwd", _ptr(x), _ptr(y), x.numel(), _stream(stream))
+    return y
+
+
+def gelu_bwd(x, dy, dx=None, stream=None):
+    dx = torch.empty_like(x) if dx is None else dx
+    _lib.call("vit_gelu_bwd", _ptr(x), _ptr(dy), _ptr(dx), x.numel(), _stream(stream))
+    return dx
+
+
+def softmax_xent(logits, labels, stream=None):
+    """Returns (loss [1] f32, dlogits [rows, classes] f32 = d(mean loss)/dlogits)."""
+    _need_cuda(logits, labels)
+    rows, classes = logits.shape
+    loss = torch.empty(1, dtype=torch.float32, device=logits.device)
+    dlogits = torch.empty_like(logits)
+    ws = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    _lib.call("vit_softmax_xent", _ptr(logits), _ptr(labels), rows, classes, _ptr(loss), _ptr(dlogits), _ptr(ws),
+              _stream(stream))
+    return loss, dlogits
+
+
+def adamw(table_dev, nchunks, lr, beta1, beta2, eps, weight_decay, bias_corr1, bias_corr2, grad_scale,
+          shadow_dtype, stream=None):
+    _lib.call("vit_adamw", _ptr(table_dev), nchunks, lr, beta1, beta2, eps, weight_decay, bias_corr1, bias_corr2,
+              grad_scale, dtype_code(shadow_dtype), _stream(stream))
+
+
+def pack(table_dev, nchunks, shadow_dtype, stream=None):
+    _lib.call("vit_pack", _ptr(table_dev), nchunks, dtype_code(shadow_dtype), _stream(stream))
+
+
+CHUNK = 65536
+
+
+def build_chunk_table(entries, device):
+    """entries: list of (p, g, m, v, shadow) tensors (fp32 contiguous, shadow may be None).  Returns (uint8 device
+    tensor holding the vit_tensor_chunk array, nchunks)."""
+    chunks = []
+    for p, g, m, v, sh in entries:
+        n = p.numel()
+        es = sh.element_size() if sh is not None else 0
+        for off in range(0, n, CHUNK):
+            c = _lib.TensorChunk()
+            c.p = p.data_ptr() + 4 * off
+            c.g = (g.data_ptr() + 4 * off) if g is not None else 0
+            c.m = (m.data_ptr() + 4 * off) if m is not None else 0
+            c.v = (v.data_ptr() + 4 * off) if v is not None else 0
+            c.shadow = (sh.data_ptr() + es * off) if sh is not None else None
+            c.n = min(CHUNK, n - off)
+            chunks.append(c)
+    arr = (_lib.TensorChunk * len(chunks))(*chunks)
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return host.to(device), len(chunks)

@@ -1,0 +1,599 @@
+// Multi-head self-attention forward/backward for the ViT encoder (transformer.py:9-31, :44-45).
+// Reference semantics: logits are MULTIPLIED by sqrt(hd) (`scale` argument), no mask, softmax over keys.
+//
+// qkv[B*T][3D]: Q at column h*hd, K at D + h*hd, V at 2D + h*hd.  o[B*T][D].  lse[B][H][T] (natural log).
+//
+// bf16, hd == 64 — flash-style MFMA kernels (v_mfma_f32_32x32x16_bf16, wave64):
+//   forward: workgroup = 4 waves x 32 queries; K/V tiles of 64 keys double-buffered in LDS; S^T = K.Q^T so each lane
+//   owns one query's column (softmax statistics are per-lane scalars), P^T is reused in registers as the B operand
+//   of O^T = V^T.P^T (no LDS round trip for P); V^T fragments come from ds_read_b64_tr_b16 transposed reads.
+//   backward: dQ kernel (queries on lanes, K/V streamed) and dK/dV kernel (keys on lanes, Q/dO streamed); P is
+//   recomputed from the saved LSE; no atomics, deterministic.
+//   LDS images are [row][64 bf16] with a 16-B chunk XOR swizzle that is conflict-free for both the ds_read_b128 row
+//   reads and the transposed reads.
+// Other dtypes / head sizes — generic VALU kernels (exact fp32 arithmetic order per row), also used when the
+// `.attention_probs` tensor is requested.
+#include "vit_common.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+// ===============================================================================================================
+// Generic VALU kernels
+// ===============================================================================================================
+constexpr int GA_TMAX = 2048;
+constexpr int GA_HDMAX = 128;
+
+template <class T>
+__global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ qkv, T* __restrict__ o,
+                                                        float* __restrict__ lse, float* __restrict__ probs, int64_t B,
+                                                        int64_t Tn, int64_t H, int64_t hd, float scale) {
+  __shared__ float sc[4][GA_TMAX];
+  __shared__ float qs[4][GA_HDMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int64_t qv = (int64_t)blockIdx.x * 4 + w;
+  const bool valid = qv < Tn;          // no early exit: every wave reaches the barriers
+  const int64_t q = valid ? qv : Tn - 1;
+  const int64_t D = H * hd, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld;
+  for (int d = lane; d < hd; d += 64) qs[w][d] = ld1<T>(base + q * ld + h * hd + d);
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int64_t j = lane; j < Tn; j += 64) {
+    const T* kr = base + j * ld + D + h * hd;
+    float s = 0.f;
+    for (int d = 0; d < hd; ++d) s += qs[w][d] * ld1<T>(kr + d);
+    s *= scale;
+    sc[w][j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float l = 0.f;
+  for (int64_t j = lane; j < Tn; j += 64) {
+    const float p = expf(sc[w][j] - mx);
+    sc[w][j] = p;
+    l += p;
+  }
+  l = wave_sum(l);
+  const float inv = 1.0f / l;
+  for (int64_t j = lane; j < Tn; j += 64) {
+    const float p = sc[w][j] * inv;
+    sc[w][j] = p;
+    if (probs && valid) probs[(bh * Tn + q) * Tn + j] = p;
+  }
+  __syncthreads();
+  for (int d = lane; d < hd; d += 64) {
+    float acc = 0.f;
+    for (int64_t j = 0; j < Tn; ++j) acc += sc[w][j] * ld1<T>(base + j * ld + 2 * D + h * hd + d);
+    if (valid) st1<T>(o + (b * Tn + q) * D + h * hd + d, acc);
+  }
+  if (lane == 0 && valid) lse[bh * Tn + q] = mx + logf(l);
+}
+
+// Backward A: one wave per query row: P, dP, dS rows (dS and P to workspace) and the dQ row.
+template <class T>
+__global__ __launch_bounds__(256) void attn_bwd_generic_rows(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                             const T* __restrict__ d_o, const float* __restrict__ lse,
+                                                             T* __restrict__ dqkv, float* __restrict__ Pws,
+                                                             float* __restrict__ dSws, int64_t B, int64_t Tn,
+                                                             int64_t H, int64_t hd, float scale) {
+  __shared__ float ds_s[4][GA_TMAX];
+  __shared__ float qs[4][GA_HDMAX];
+  __shared__ float dos[4][GA_HDMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int64_t qv = (int64_t)blockIdx.x * 4 + w;
+  const bool valid = qv < Tn;
+  const int64_t q = valid ? qv : Tn - 1;
+  const int64_t D = H * hd, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld;
+  float dl = 0.f;
+  for (int d = lane; d < hd; d += 64) {
+    qs[w][d] = ld1<T>(base + q * ld + h * hd + d);
+    const float g = ld1<T>(d_o + (b * Tn + q) * D + h * hd + d);
+    dos[w][d] = g;
+    dl += g * ld1<T>(o + (b * Tn + q) * D + h * hd + d);
+  }
+  dl = wave_sum(dl);
+  __syncthreads();
+  const float L = lse[bh * Tn + q];
+  for (int64_t j = lane; j < Tn; j += 64) {
+    const T* kr = base + j * ld + D + h * hd;
+    const T* vr = base + j * ld + 2 * D + h * hd;
+    float s = 0.f, dp = 0.f;
+    for (int d = 0; d < hd; ++d) {
+      s += qs[w][d] * ld1<T>(kr + d);
+      dp += dos[w][d] * ld1<T>(vr + d);
+    }
+    const float p = expf(s * scale - L);
+    const float ds = p * (dp - dl);
+    ds_s[w][j] = ds;
+    if (valid) {
+      Pws[(bh * Tn + q) * Tn + j] = p;
+      dSws[(bh * Tn + q) * Tn + j] = ds;
+    }
+  }
+  __syncthreads();
+  for (int d = lane; d < hd; d += 64) {
+    float acc = 0.f;
+    for (int64_t j = 0; j < Tn; ++j) acc += ds_s[w][j] * ld1<T>(base + j * ld + D + h * hd + d);
+    if (valid) st1<T>(dqkv + (b * Tn + q) * ld + h * hd + d, acc * scale);
+  }
+}
+
+// Backward B: one wave per key row: dK row = scale * sum_q dS[q][j] Q[q], dV row = sum_q P[q][j] dO[q].
+template <class T>
+__global__ __launch_bounds__(256) void attn_bwd_generic_cols(const T* __restrict__ qkv, const T* __restrict__ d_o,
+                                                             T* __restrict__ dqkv, const float* __restrict__ Pws,
+                                                             const float* __restrict__ dSws, int64_t B, int64_t Tn,
+                                                             int64_t H, int64_t hd, float scale) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int64_t j = (int64_t)blockIdx.x * 4 + w;
+  if (j >= Tn) return;
+  const int64_t D = H * hd, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld;
+  for (int d = lane; d < hd; d += 64) {
+    float dk = 0.f, dv = 0.f;
+    for (int64_t q = 0; q < Tn; ++q) {
+      const float ds = dSws[(bh * Tn + q) * Tn + j];
+      const float p = Pws[(bh * Tn + q) * Tn + j];
+      dk += ds * ld1<T>(base + q * ld + h * hd + d);
+      dv += p * ld1<T>(d_o + (b * Tn + q) * D + h * hd + d);
+    }
+    st1<T>(dqkv + (b * Tn + j) * ld + D + h * hd + d, dk * scale);
+    st1<T>(dqkv + (b * Tn + j) * ld + 2 * D + h * hd + d, dv);
+  }
+}
+
+// ===============================================================================================================
+// bf16, hd = 64 MFMA kernels
+// ===============================================================================================================
+constexpr int HD = 64;
+constexpr int KT = 64;                 // keys (or queries) per streamed LDS tile
+constexpr int TILE = KT * HD;          // 4096 bf16 = 8 KiB
+
+VIT_DEV int aswz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+
+typedef short s16x4_lds __attribute__((ext_vector_type(4)));
+VIT_DEV s16x4 tr_read(const bf16_t* p) {
+  typedef __attribute__((address_space(3))) s16x4_lds* lds_ptr_t;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ptr_t)p);
+}
+
+// Stage a 64-row x 64-col bf16 tile (rows r0.., columns col0..col0+63 of a row-major matrix with leading dim ld,
+// rows >= nrows zero-filled) through registers.
+VIT_DEV void tile_load(const bf16_t* __restrict__ src, int64_t ld, int64_t r0, int64_t nrows, int64_t col0, int tid,
+                       uint4 (&reg)[2]) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int q = tid + 256 * it;
+    const int64_t r = r0 + (q >> 3);
+    const int c = q & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < nrows) v = *reinterpret_cast<const uint4*>(src + r * ld + col0 + c * 8);
+    reg[it] = v;
+  }
+}
+VIT_DEV void tile_store(bf16_t* lds, int tid, const uint4 (&reg)[2]) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int q = tid + 256 * it;
+    const int r = q >> 3, c = q & 7;
+    *reinterpret_cast<uint4*>(lds + r * HD + ((c ^ aswz(r)) << 3)) = reg[it];
+  }
+}
+
+// 32x32x16 operand fragment from a [row][64] tile, rows rb..rb+31, k-step s (d = 16s..16s+15):
+// lane holds X[rb + (lane&31)][16s + 8(lane>>5) + 0..7]
+VIT_DEV bf16x8_t row_frag(const bf16_t* t, int rb, int s, int lane) {
+  const int r = rb + (lane & 31);
+  const int c = 2 * s + (lane >> 5);
+  s16x8 v = *reinterpret_cast<const s16x8*>(t + r * HD + ((c ^ aswz(r)) << 3));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// Transposed fragment: A operand of Y[d][x] += sum_row X^T... i.e. lane (row d = db*32 + (lane&31), half h) element j
+// = t[rb + 8(j>>2) + 4h + (j&3)][db*32 + (lane&31)] — matches the k order of an accumulator used as B operand.
+VIT_DEV bf16x8_t tr_frag(const bf16_t* t, int rb, int db, int lane) {
+  const int G = lane >> 4, hh = G >> 1, lg = lane & 15, q = lg >> 2, p = lg & 3;
+  const int r1 = rb + 4 * hh + q, r2 = r1 + 8;
+  const int col = db * 32 + 16 * (G & 1) + 4 * p;
+  const int c = col >> 3;
+  s16x4 lo = tr_read(t + r1 * HD + ((c ^ aswz(r1)) << 3) + (p & 1) * 4);
+  s16x4 hi = tr_read(t + r2 * HD + ((c ^ aswz(r2)) << 3) + (p & 1) * 4);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// Fragment straight from global: lane holds X[row0 + (lane&31)][col0 + 16s + 8(lane>>5) + 0..7] (zero past nrows)
+VIT_DEV bf16x8_t glb_frag(const bf16_t* __restrict__ src, int64_t ld, int64_t row0, int64_t nrows, int64_t col0,
+                          int s, int lane) {
+  const int64_t r = row0 + (lane & 31);
+  s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (r < nrows) v = *reinterpret_cast<const s16x8*>(src + r * ld + col0 + 16 * s + 8 * (lane >> 5));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// 8 consecutive accumulator registers (8s2 .. 8s2+7) -> bf16 B fragment
+VIT_DEV bf16x8_t pack8(const float* x) {
+  s16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(x[j]);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+VIT_DEV f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// row index (within a 32-row MFMA tile) of accumulator register r for lane half h
+VIT_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                     float* __restrict__ lse, int64_t Tn, int64_t H, float scale) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];  // [buf][K,V]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int64_t D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + b * Tn * ld;
+  const int64_t q0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const float c2 = scale * LOG2E;
+
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = glb_frag(base, ld, q0, Tn, h * HD, s, lane);
+
+  f32x16 oacc[2] = {f32x16{}, f32x16{}};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int ntiles = (int)((Tn + KT - 1) / KT);
+  uint4 rk[2], rv[2];
+  tile_load(base, ld, 0, Tn, D + h * HD, tid, rk);
+  tile_load(base, ld, 0, Tn, 2 * D + h * HD, tid, rv);
+  tile_store(smem, tid, rk);
+  tile_store(smem + TILE, tid, rv);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, D + h * HD, tid, rk);
+      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, 2 * D + h * HD, tid, rv);
+    }
+    const bf16_t* Ks = smem + cur * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = sub * 32;
+      f32x16 sacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sacc = mfma32(row_frag(Ks, kb, s, lane), qf[s], sacc);
+      const int64_t key0 = (int64_t)t * KT + kb;
+      float x[16];
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t key = key0 + acc_row(r, hf);
+        x[r] = key < Tn ? sacc[r] * c2 : -INFINITY;
+        mloc = fmaxf(mloc, x[r]);
+      }
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      const float m_new = fmaxf(m_run, mloc);
+      const float alpha = exp2f(m_run - m_new);
+      float psum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        x[r] = exp2f(x[r] - m_new);
+        psum += x[r];
+      }
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+      oacc[0] *= alpha;
+      oacc[1] *= alpha;
+      const bf16x8_t pb0 = pack8(x), pb1 = pack8(x + 8);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        oacc[db] = mfma32(tr_frag(Vs, kb, db, lane), pb0, oacc[db]);
+        oacc[db] = mfma32(tr_frag(Vs, kb + 16, db, lane), pb1, oacc[db]);
+      }
+    }
+    if (more) {
+      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;
+      tile_store(nb, tid, rk);
+      tile_store(nb + TILE, tid, rv);
+    }
+    __syncthreads();
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  const int64_t q = q0 + (lane & 31);
+  if (q < Tn) {
+    bf16_t* orow = o + (b * Tn + q) * D + h * HD;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4] = {oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv, oacc[db][4 * g + 2] * inv,
+                      oacc[db][4 * g + 3] * inv};
+        st4<bf16_t>(orow + db * 32 + 8 * g + 4 * hf, v);
+      }
+    }
+    if (hf == 0) lse[bh * Tn + q] = (m_run + log2f(l_tot)) / LOG2E;
+  }
+}
+
+// delta[b,h,q] = sum_d dO . O  (fp32), one thread per (row, head)
+__global__ __launch_bounds__(256) void attn_delta(const bf16_t* __restrict__ o, const bf16_t* __restrict__ d_o,
+                                                  float* __restrict__ delta, int64_t B, int64_t Tn, int64_t H) {
+  const int64_t total = B * Tn * H;
+  const int64_t D = H * HD;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = t / H, h = t % H, b = row / Tn, q = row % Tn;
+    const bf16_t* a = o + row * D + h * HD;
+    const bf16_t* g = d_o + row * D + h * HD;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < HD; c += 8) {
+      s16x8 va = *reinterpret_cast<const s16x8*>(a + c);
+      s16x8 vg = *reinterpret_cast<const s16x8*>(g + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += bf2f((bf16_t)va[j]) * bf2f((bf16_t)vg[j]);
+    }
+    delta[(b * H + h) * Tn + q] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ d_o,
+                                                        const float* __restrict__ lse, const float* __restrict__ delta,
+                                                        bf16_t* __restrict__ dqkv, int64_t Tn, int64_t H, float scale) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int64_t D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + b * Tn * ld;
+  const int64_t q0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const int64_t q = q0 + (lane & 31);
+  const float c2 = scale * LOG2E;
+  bf16x8_t qf[4], gf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = glb_frag(base, ld, q0, Tn, h * HD, s, lane);
+    gf[s] = glb_frag(d_o + b * Tn * D, D, q0, Tn, h * HD, s, lane);
+  }
+  const float lse2 = q < Tn ? lse[bh * Tn + q] * LOG2E : 0.f;
+  const float dl = q < Tn ? delta[bh * Tn + q] : 0.f;
+  f32x16 dq[2] = {f32x16{}, f32x16{}};
+  const int ntiles = (int)((Tn + KT - 1) / KT);
+  uint4 rk[2], rv[2];
+  tile_load(base, ld, 0, Tn, D + h * HD, tid, rk);
+  tile_load(base, ld, 0, Tn, 2 * D + h * HD, tid, rv);
+  tile_store(smem, tid, rk);
+  tile_store(smem + TILE, tid, rv);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, D + h * HD, tid, rk);
+      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, 2 * D + h * HD, tid, rv);
+    }
+    const bf16_t* Ks = smem + cur * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = sub * 32;
+      f32x16 sacc = {}, pacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(row_frag(Ks, kb, s, lane), qf[s], sacc);
+        pacc = mfma32(row_frag(Vs, kb, s, lane), gf[s], pacc);
+      }
+      const int64_t key0 = (int64_t)t * KT + kb;
+      float ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t key = key0 + acc_row(r, hf);
+        const float p = key < Tn ? exp2f(sacc[r] * c2 - lse2) : 0.f;
+        ds[r] = p * (pacc[r] - dl);
+      }
+      const bf16x8_t d0 = pack8(ds), d1 = pack8(ds + 8);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dq[db] = mfma32(tr_frag(Ks, kb, db, lane), d0, dq[db]);
+        dq[db] = mfma32(tr_frag(Ks, kb + 16, db, lane), d1, dq[db]);
+      }
+    }
+    if (more) {
+      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;
+      tile_store(nb, tid, rk);
+      tile_store(nb + TILE, tid, rv);
+    }
+    __syncthreads();
+  }
+  if (q < Tn) {
+    bf16_t* dst = dqkv + (b * Tn + q) * ld + h * HD;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4] = {dq[db][4 * g] * scale, dq[db][4 * g + 1] * scale, dq[db][4 * g + 2] * scale,
+                      dq[db][4 * g + 3] * scale};
+        st4<bf16_t>(dst + db * 32 + 8 * g + 4 * hf, v);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv,
+                                                          const bf16_t* __restrict__ d_o,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                          int64_t Tn, int64_t H, float scale) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];  // [buf][Q, dO]
+  __shared__ float stat[2][2][KT];                                     // [buf][lse2, delta]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int64_t D = H * HD, ld = 3 * D;
+  const bf16_t* base = qkv + b * Tn * ld;
+  const bf16_t* gbase = d_o + b * Tn * D;
+  const int64_t k0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const float c2 = scale * LOG2E;
+  bf16x8_t kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = glb_frag(base, ld, k0, Tn, D + h * HD, s, lane);
+    vf[s] = glb_frag(base, ld, k0, Tn, 2 * D + h * HD, s, lane);
+  }
+  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+  const int ntiles = (int)((Tn + KT - 1) / KT);
+  uint4 rq[2], rg[2];
+  float st_l = 0.f, st_d = 0.f;
+  auto load_stats = [&](int t) {
+    if (tid < KT) {
+      const int64_t qq = (int64_t)t * KT + tid;
+      st_l = qq < Tn ? lse[bh * Tn + qq] * LOG2E : 0.f;
+      st_d = qq < Tn ? delta[bh * Tn + qq] : 0.f;
+    }
+  };
+  tile_load(base, ld, 0, Tn, h * HD, tid, rq);
+  tile_load(gbase, D, 0, Tn, h * HD, tid, rg);
+  load_stats(0);
+  tile_store(smem, tid, rq);
+  tile_store(smem + TILE, tid, rg);
+  if (tid < KT) {
+    stat[0][0][tid] = st_l;
+    stat[0][1][tid] = st_d;
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, h * HD, tid, rq);
+      tile_load(gbase, D, (int64_t)(t + 1) * KT, Tn, h * HD, tid, rg);
+      load_stats(t + 1);
+    }
+    const bf16_t* Qs = smem + cur * 2 * TILE;
+    const bf16_t* Gs = Qs + TILE;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qb = sub * 32;
+      f32x16 sacc = {}, pacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(row_frag(Qs, qb, s, lane), kf[s], sacc);   // S[q][key]
+        pacc = mfma32(row_frag(Gs, qb, s, lane), vf[s], pacc);   // dP[q][key]
+      }
+      const int64_t qrow0 = (int64_t)t * KT + qb;
+      float p[16], ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = qb + acc_row(r, hf);
+        const float l2 = stat[cur][0][qr], dlt = stat[cur][1][qr];
+        const bool valid = qrow0 + acc_row(r, hf) < Tn;
+        p[r] = valid ? exp2f(sacc[r] * c2 - l2) : 0.f;
+        ds[r] = p[r] * (pacc[r] - dlt);
+      }
+      const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dv[db] = mfma32(tr_frag(Gs, qb, db, lane), p0, dv[db]);
+        dv[db] = mfma32(tr_frag(Gs, qb + 16, db, lane), p1, dv[db]);
+        dk[db] = mfma32(tr_frag(Qs, qb, db, lane), d0, dk[db]);
+        dk[db] = mfma32(tr_frag(Qs, qb + 16, db, lane), d1, dk[db]);
+      }
+    }
+    if (more) {
+      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;
+      tile_store(nb, tid, rq);
+      tile_store(nb + TILE, tid, rg);
+      if (tid < KT) {
+        stat[cur ^ 1][0][tid] = st_l;
+        stat[cur ^ 1][1][tid] = st_d;
+      }
+    }
+    __syncthreads();
+  }
+  const int64_t key = k0 + (lane & 31);
+  if (key < Tn) {
+    bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD;
+    bf16_t* dvr = dkr + D;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
+                      dk[db][4 * g + 3] * scale};
+        float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+        st4<bf16_t>(dkr + db * 32 + 8 * g + 4 * hf, a);
+        st4<bf16_t>(dvr + db * 32 + 8 * g + 4 * hf, c);
+      }
+    }
+  }
+}
+
+bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }
+
+}  // namespace
+
+extern "C" int vit_attn_fwd(const void* qkv, void* o, float* lse, float* probs, int64_t B, int64_t T, int64_t H,
+                            int64_t hd, float scale, int32_t dtype, void* stream) {
+  VIT_REQUIRE(qkv && o && lse && B > 0 && T > 0 && H > 0 && hd > 0, "vit_attn_fwd: bad arguments");
+  hipStream_t s = VIT_STREAM(stream);
+  if (use_mfma(dtype, hd) && probs == nullptr) {
+    VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
+    dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
+    attn_fwd_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, scale);
+  } else {
+    VIT_REQUIRE(T <= GA_TMAX && hd <= GA_HDMAX, "vit_attn_fwd(generic): T<=%d, hd<=%d", GA_TMAX, GA_HDMAX);
+    dim3 grid((unsigned)((T + 3) / 4), (unsigned)(B * H));
+    if (dtype == VIT_BF16)
+      attn_fwd_generic<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, probs, B, T, H, hd, scale);
+    else
+      attn_fwd_generic<float><<<grid, 256, 0, s>>>((const float*)qkv, (float*)o, lse, probs, B, T, H, hd, scale);
+  }
+  return vit::check_launch("vit_attn_fwd");
+}
+
+extern "C" int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype) {
+  if (use_mfma(dtype, hd)) return B * H * T * (int64_t)sizeof(float);
+  return 2 * B * H * T * T * (int64_t)sizeof(float);
+}
+
+extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, const float* lse, void* dqkv, int64_t B,
+                            int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace,
+                            void* stream) {
+  VIT_REQUIRE(qkv && o && d_o && lse && dqkv && workspace && B > 0 && T > 0 && H > 0 && hd > 0,
+              "vit_attn_bwd: bad arguments");
+  hipStream_t s = VIT_STREAM(stream);
+  if (use_mfma(dtype, hd)) {
+    float* delta = (float*)workspace;
+    const int64_t rows = B * T * H;
+    attn_delta<<<(unsigned)std::min<int64_t>((rows + 255) / 256, 8192), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)d_o,
+                                                                                 delta, B, T, H);
+    dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
+    attn_bwd_dq_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
+                                          scale);
+    attn_bwd_dkdv_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
+                                            scale);
+  } else {
+    VIT_REQUIRE(T <= GA_TMAX && hd <= GA_HDMAX, "vit_attn_bwd(generic): T<=%d, hd<=%d", GA_TMAX, GA_HDMAX);
+    float* Pws = (float*)workspace;
+    float* dSws = Pws + B * H * T * T;
+    dim3 grid((unsigned)((T + 3) / 4), (unsigned)(B * H));
+    if (dtype == VIT_BF16) {
+      attn_bwd_generic_rows<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse,
+                                                         (bf16_t*)dqkv, Pws, dSws, B, T, H, hd, scale);
+      attn_bwd_generic_cols<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, (bf16_t*)dqkv, Pws,
+                                                         dSws, B, T, H, hd, scale);
+    } else {
+      attn_bwd_generic_rows<float><<<grid, 256, 0, s>>>((const float*)qkv, (const float*)o, (const float*)d_o, lse,
+                                                        (float*)dqkv, Pws, dSws, B, T, H, hd, scale);
+      attn_bwd_generic_cols<float><<<grid, 256, 0, s>>>((const float*)qkv, (const float*)d_o, (float*)dqkv, Pws, dSws,
+                                                        B, T, H, hd, scale);
+    }
+  }
+  return vit::check_launch("vit_attn_bwd");
+}

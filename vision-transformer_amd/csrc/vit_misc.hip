@@ -1,0 +1,368 @@
+// Memory-bound kernels of the ViT step: patch im2col, CLS rows, column sums, strided copies, dropout backward,
+// GELU, softmax cross-entropy, and the multi-tensor AdamW / shadow-weight pack.  All vectorised where the shape
+// allows (8-16 B per lane), grid-stride, fixed reduction order (bitwise reproducible).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "vit_common.h"
+
+namespace vit {
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return VIT_ERR_LAUNCH;
+  }
+  return VIT_OK;
+}
+}  // namespace vit
+
+extern "C" int vit_abi_version(void) { return VIT_ABI_VERSION; }
+extern "C" const char* vit_last_error(void) { return vit::g_err; }
+
+namespace {
+
+inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap = 8192) {
+  int64_t b = (work + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (unsigned)b;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// im2col: one thread per (row m = b*N + n, 4 consecutive columns); column (c, kh, kw) with kw fastest.
+// ---------------------------------------------------------------------------------------------------------------
+template <class TI, class TO>
+__global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ x, TO* __restrict__ cols, int64_t B,
+                                                     int64_t C, int64_t H, int64_t W, int64_t P) {
+  const int64_t nw = W / P, nh = H / P, N = nh * nw, KC = C * P * P;
+  const int64_t q4 = KC / 4, total = B * N * q4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = t / q4, col = (t % q4) * 4;
+    const int64_t b = m / N, n = m % N, ph = n / nw, pw = n % nw;
+    const int64_t c = col / (P * P), rem = col % (P * P), kh = rem / P, kw = rem % P;
+    const TI* src = x + ((b * C + c) * H + ph * P + kh) * W + pw * P + kw;
+    float v[4];
+    v[0] = ld1<TI>(src); v[1] = ld1<TI>(src + 1); v[2] = ld1<TI>(src + 2); v[3] = ld1<TI>(src + 3);
+    st4<TO>(cols + m * KC + col, v);
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void embed_cls_kernel(const float* __restrict__ cls, const float* __restrict__ pos,
+                                                        T* __restrict__ x0, int64_t B, int64_t T_, int64_t D) {
+  const int64_t N = T_ - 1;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < B * D; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / D, d = t % D;
+    st1<T>(x0 + (b * T_ + N) * D + d, cls[b * D + d] + pos[N * D + d]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Column sums, two deterministic stages.  Stage 1: block (64 x 4 threads) owns 256 columns (4 per lane) and a chunk
+// of rows; writes partial[chunk][cols].  Stage 2: one thread per column sums the chunks in order.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int CS_CHUNKS_MAX = 256;
+
+template <class T>
+__global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ x, int64_t ldx, int64_t rows,
+                                                     int64_t cols, int64_t rows_per_chunk, float* __restrict__ part,
+                                                     int vec) {
+  __shared__ float red[4][256];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 256 + tx * 4;
+  const int64_t chunk = blockIdx.y;
+  const int64_t r0 = chunk * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0 + ty; r < r1; r += 4) {
+    const T* p = x + r * ldx + c0;
+    if (vec && c0 + 3 < cols) {
+      float v[4];
+      ld4<T>(p, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += v[k];
+    } else {
+      for (int k = 0; k < 4; ++k)
+        if (c0 + k < cols) acc[k] += ld1<T>(p + k);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[ty][tx * 4 + k] = acc[k];
+  __syncthreads();
+  if (ty == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cc = tx * 4 + k;
+      const float s = red[0][cc] + red[1][cc] + red[2][cc] + red[3][cc];
+      if (c0 + k < cols) part[chunk * cols + c0 + k] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int64_t nchunks, int64_t cols,
+                                                     float* __restrict__ out, float beta) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < cols; c += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int64_t k = 0; k < nchunks; ++k) s += part[k * cols + c];
+    out[c] = beta != 0.f ? beta * out[c] + s : s;
+  }
+}
+
+int64_t colsum_chunks(int64_t rows, int64_t cols) {
+  // aim for ~2048 blocks total, each with >= 32 rows
+  const int64_t cblocks = (cols + 255) / 256;
+  int64_t ch = 2048 / (cblocks > 0 ? cblocks : 1);
+  if (ch < 1) ch = 1;
+  if (ch > CS_CHUNKS_MAX) ch = CS_CHUNKS_MAX;
+  const int64_t maxch = (rows + 31) / 32;
+  if (ch > maxch) ch = maxch;
+  if (ch < 1) ch = 1;
+  return ch;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+template <class TS, class TD>
+__global__ __launch_bounds__(256) void copy2d_kernel(const TS* __restrict__ src, int64_t lds, TD* __restrict__ dst,
+                                                     int64_t ldd, int64_t rows, int64_t cols, int64_t grp,
+                                                     int64_t grp_stride, float beta) {
+  const int64_t total = rows * cols;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / cols, j = t % cols;
+    const int64_t si = grp ? (i / grp) * grp_stride + (i % grp) : i;
+    float v = ld1<TS>(src + si * lds + j);
+    TD* d = dst + i * ldd + j;
+    if (beta != 0.f) v += beta * ld1<TD>(d);
+    st1<TD>(d, v);
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
+                                                          uint32_t thr, float scale, uint32_t seed) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    const float v = ld1<T>(x + t);
+    st1<T>(y + t, vit_hash_u32(seed, (uint32_t)t) >= thr ? v * scale : 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    y[t] = gelu_erf(x[t]);
+}
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                       float* __restrict__ dx, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    dx[t] = dy[t] * gelu_erf_grad(x[t]);
+}
+
+// one workgroup per row: max, sum-exp, loss term, gradient row
+__global__ __launch_bounds__(256) void xent_rows_kernel(const float* __restrict__ logits,
+                                                        const int64_t* __restrict__ labels, int64_t classes,
+                                                        float inv_rows, float* __restrict__ dlogits,
+                                                        float* __restrict__ row_loss) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const float* x = logits + r * classes;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float mx = -INFINITY;
+  for (int64_t c = tid; c < classes; c += 256) mx = fmaxf(mx, x[c]);
+  mx = wave_max(mx);
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int64_t c = tid; c < classes; c += 256) s += __expf(x[c] - mx);
+  s = wave_sum(s);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  const float lse = mx + __logf(s);
+  const int64_t y = labels[r];
+  for (int64_t c = tid; c < classes; c += 256) {
+    const float p = __expf(x[c] - lse);
+    dlogits[r * classes + c] = (p - (c == y ? 1.f : 0.f)) * inv_rows;
+  }
+  if (tid == 0) row_loss[r] = lse - x[y];
+}
+
+__global__ __launch_bounds__(256) void xent_reduce_kernel(const float* __restrict__ row_loss, int64_t rows,
+                                                          float inv_rows, float* __restrict__ loss) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) s += row_loss[r];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *loss = (red[0] + red[1] + red[2] + red[3]) * inv_rows;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Multi-tensor AdamW: one workgroup per table chunk (<= 64 Ki elements), 4 elements per lane per step.
+// ---------------------------------------------------------------------------------------------------------------
+template <class TS>
+__global__ __launch_bounds__(256) void adamw_kernel(const vit_tensor_chunk* __restrict__ tab, float lr, float b1,
+                                                    float b2, float eps, float wd, float step_size,
+                                                    float inv_sqrt_bc2, float gscale) {
+  const vit_tensor_chunk ch = tab[blockIdx.x];
+  const float decay = 1.0f - lr * wd;
+  for (int64_t t = threadIdx.x; t < ch.n; t += 256) {
+    float g = ch.g[t] * gscale;
+    float m = ch.m[t], v = ch.v[t], p = ch.p[t];
+    p *= decay;
+    m = b1 * m + (1.0f - b1) * g;
+    v = b2 * v + (1.0f - b2) * g * g;
+    const float denom = sqrtf(v) * inv_sqrt_bc2 + eps;
+    p -= step_size * (m / denom);
+    ch.m[t] = m;
+    ch.v[t] = v;
+    ch.p[t] = p;
+    if (ch.shadow) st1<TS>((TS*)ch.shadow + t, p);
+  }
+}
+
+template <class TS>
+__global__ __launch_bounds__(256) void pack_kernel(const vit_tensor_chunk* __restrict__ tab) {
+  const vit_tensor_chunk ch = tab[blockIdx.x];
+  if (!ch.shadow) return;
+  for (int64_t t = threadIdx.x; t < ch.n; t += 256) st1<TS>((TS*)ch.shadow + t, ch.p[t]);
+}
+
+}  // namespace
+
+// ===============================================================================================================
+extern "C" int vit_im2col(const void* x, int32_t x_dtype, void* cols, int32_t dtype, int64_t B, int64_t C, int64_t H,
+                          int64_t W, int64_t P, void* stream) {
+  VIT_REQUIRE(x && cols, "vit_im2col: null pointer");
+  VIT_REQUIRE(B > 0 && C > 0 && P > 0 && H % P == 0 && W % P == 0, "vit_im2col: image %lldx%lld not divisible by P=%lld",
+              (long long)H, (long long)W, (long long)P);
+  VIT_REQUIRE(P % 4 == 0, "vit_im2col: patch size must be a multiple of 4");
+  const int64_t work = B * (H / P) * (W / P) * C * P * P / 4;
+  const unsigned grid = grid_for(work, 256, 16384);
+  hipStream_t s = VIT_STREAM(stream);
+  if (x_dtype == VIT_F32 && dtype == VIT_BF16)
+    im2col_kernel<float, bf16_t><<<grid, 256, 0, s>>>((const float*)x, (bf16_t*)cols, B, C, H, W, P);
+  else if (x_dtype == VIT_F32 && dtype == VIT_F32)
+    im2col_kernel<float, float><<<grid, 256, 0, s>>>((const float*)x, (float*)cols, B, C, H, W, P);
+  else if (x_dtype == VIT_BF16 && dtype == VIT_BF16)
+    im2col_kernel<bf16_t, bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)cols, B, C, H, W, P);
+  else {
+    vit::set_error("vit_im2col: unsupported dtype pair %d->%d", x_dtype, dtype);
+    return VIT_ERR_INVALID;
+  }
+  return vit::check_launch("vit_im2col");
+}
+
+extern "C" int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, int64_t B, int64_t T,
+                             int64_t D, void* stream) {
+  VIT_REQUIRE(cls && pos && x0 && B > 0 && T > 0 && D > 0, "vit_embed_cls: bad arguments");
+  const unsigned grid = grid_for(B * D, 256);
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16) embed_cls_kernel<bf16_t><<<grid, 256, 0, s>>>(cls, pos, (bf16_t*)x0, B, T, D);
+  else embed_cls_kernel<float><<<grid, 256, 0, s>>>(cls, pos, (float*)x0, B, T, D);
+  return vit::check_launch("vit_embed_cls");
+}
+
+extern "C" int64_t vit_colsum_workspace_bytes(int64_t rows, int64_t cols) {
+  return colsum_chunks(rows, cols) * cols * (int64_t)sizeof(float);
+}
+
+extern "C" int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t cols, float* out,
+                          float beta, void* workspace, void* stream) {
+  VIT_REQUIRE(x && out && workspace && rows > 0 && cols > 0, "vit_colsum: bad arguments");
+  const int64_t ch = colsum_chunks(rows, cols);
+  const int64_t rpc = (rows + ch - 1) / ch;
+  const int vec = (cols % 4 == 0) && (ldx % 4 == 0) && (((uintptr_t)x) % 16 == 0);
+  dim3 g1((unsigned)((cols + 255) / 256), (unsigned)ch);
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16)
+    colsum_stage1<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
+  else
+    colsum_stage1<float><<<g1, 256, 0, s>>>((const float*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
+  colsum_stage2<<<grid_for(cols, 256), 256, 0, s>>>((const float*)workspace, ch, cols, out, beta);
+  return vit::check_launch("vit_colsum");
+}
+
+extern "C" int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,
+                          int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
+                          void* stream) {
+  VIT_REQUIRE(src && dst && rows > 0 && cols > 0, "vit_copy2d: bad arguments");
+  const unsigned grid = grid_for(rows * cols, 256, 16384);
+  hipStream_t s = VIT_STREAM(stream);
+#define CP(TS, TD)                                                                                            \
+  copy2d_kernel<TS, TD><<<grid, 256, 0, s>>>((const TS*)src, lds, (TD*)dst, ldd, rows, cols, src_group_rows, \
+                                             src_group_stride, beta)
+  if (src_dtype == VIT_F32 && dst_dtype == VIT_F32) CP(float, float);
+  else if (src_dtype == VIT_F32) CP(float, bf16_t);
+  else if (dst_dtype == VIT_F32) CP(bf16_t, float);
+  else CP(bf16_t, bf16_t);
+#undef CP
+  return vit::check_launch("vit_copy2d");
+}
+
+extern "C" int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed,
+                               void* stream) {
+  VIT_REQUIRE(x && y && n > 0 && p >= 0.f && p < 1.f, "vit_dropout_bwd: bad arguments");
+  double t = (double)p * 4294967296.0;
+  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const float scale = 1.0f / (1.0f - p);
+  const unsigned grid = grid_for(n, 256, 16384);
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16) dropout_bwd_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, thr, scale, seed);
+  else dropout_bwd_kernel<float><<<grid, 256, 0, s>>>((const float*)x, (float*)y, n, thr, scale, seed);
+  return vit::check_launch("vit_dropout_bwd");
+}
+
+extern "C" int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream) {
+  VIT_REQUIRE(x && y && n > 0, "vit_gelu_fwd: bad arguments");
+  gelu_fwd_kernel<<<grid_for(n, 256), 256, 0, VIT_STREAM(stream)>>>(x, y, n);
+  return vit::check_launch("vit_gelu_fwd");
+}
+
+extern "C" int vit_gelu_bwd(const float* x, const float* dy, float* dx, int64_t n, void* stream) {
+  VIT_REQUIRE(x && dy && dx && n > 0, "vit_gelu_bwd: bad arguments");
+  gelu_bwd_kernel<<<grid_for(n, 256), 256, 0, VIT_STREAM(stream)>>>(x, dy, dx, n);
+  return vit::check_launch("vit_gelu_bwd");
+}
+
+extern "C" int vit_softmax_xent(const float* logits, const int64_t* labels, int64_t rows, int64_t classes, float* loss,
+                                float* dlogits, float* workspace, void* stream) {
+  VIT_REQUIRE(logits && labels && loss && dlogits && workspace && rows > 0 && classes > 0,
+              "vit_softmax_xent: bad arguments");
+  hipStream_t s = VIT_STREAM(stream);
+  const float inv = 1.0f / (float)rows;
+  xent_rows_kernel<<<(unsigned)rows, 256, 0, s>>>(logits, labels, classes, inv, dlogits, workspace);
+  xent_reduce_kernel<<<1, 256, 0, s>>>(workspace, rows, inv, loss);
+  return vit::check_launch("vit_softmax_xent");
+}
+
+extern "C" int vit_adamw(const vit_tensor_chunk* table_dev, int64_t nchunks, float lr, float beta1, float beta2,
+                         float eps, float weight_decay, float bias_corr1, float bias_corr2, float grad_scale,
+                         int32_t shadow_dtype, void* stream) {
+  VIT_REQUIRE(table_dev && nchunks > 0 && bias_corr1 > 0.f && bias_corr2 > 0.f, "vit_adamw: bad arguments");
+  const float step_size = lr / bias_corr1;
+  const float inv_sqrt_bc2 = 1.0f / sqrtf(bias_corr2);
+  hipStream_t s = VIT_STREAM(stream);
+  if (shadow_dtype == VIT_BF16)
+    adamw_kernel<bf16_t><<<(unsigned)nchunks, 256, 0, s>>>(table_dev, lr, beta1, beta2, eps, weight_decay, step_size,
+                                                           inv_sqrt_bc2, grad_scale);
+  else
+    adamw_kernel<float><<<(unsigned)nchunks, 256, 0, s>>>(table_dev, lr, beta1, beta2, eps, weight_decay, step_size,
+                                                          inv_sqrt_bc2, grad_scale);
+  return vit::check_launch("vit_adamw");
+}
+
+extern "C" int vit_pack(const vit_tensor_chunk* table_dev, int64_t nchunks, int32_t shadow_dtype, void* stream) {
+  VIT_REQUIRE(table_dev && nchunks > 0, "vit_pack: bad arguments");
+  hipStream_t s = VIT_STREAM(stream);
+  if (shadow_dtype == VIT_BF16) pack_kernel<bf16_t><<<(unsigned)nchunks, 256, 0, s>>>(table_dev);
+  else pack_kernel<float><<<(unsigned)nchunks, 256, 0, s>>>(table_dev);
+  return vit::check_launch("vit_pack");
+}

@@ -1,0 +1,248 @@
+// LayerNorm forward/backward (nn.LayerNorm, eps 1e-5; transformer.py:71-72,77-78 and vit.py:72).
+// One wave64 per row, the row cached in registers (NV float4 per lane, cols <= 256*NV), fp32 statistics with an
+// exact two-pass variance.  Backward fuses: residual-gradient add, the producer branch's dropout backward, and
+// per-workgroup dgamma/dbeta partials (reduced afterwards by vit_colsum in a fixed order).
+#include "vit_common.h"
+
+namespace {
+
+constexpr int LN_BWD_PARTS_MAX = 512;
+
+template <class T, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int64_t ldx,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     T* __restrict__ y, int64_t ldy, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, int64_t rows, int64_t cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + row * ldx;
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t c = ((int64_t)k * 64 + lane) * 4;
+    if (c < cols) {
+      ld4<T>(xr + c, v[k]);
+      s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+    } else {
+      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0.f;
+    }
+  }
+  const float mu = wave_sum(s) / (float)cols;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t c = ((int64_t)k * 64 + lane) * 4;
+    if (c < cols) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = v[k][r] - mu;
+        q += d * d;
+      }
+    }
+  }
+  const float var = wave_sum(q) / (float)cols;
+  const float rs = rsqrtf(var + eps);
+  T* yr = y + row * ldy;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t c = ((int64_t)k * 64 + lane) * 4;
+    if (c < cols) {
+      float g[4], b[4], o[4];
+      ld4<float>(gamma + c, g);
+      ld4<float>(beta + c, b);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (v[k][r] - mu) * rs * g[r] + b[r];
+      st4<T>(yr + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+template <class T, int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
+                                                     int64_t ldx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const T* __restrict__ dres, T* __restrict__ dx_out,
+                                                     T* __restrict__ drop_out, uint32_t drop_thr, float drop_scale,
+                                                     uint32_t drop_seed, float* __restrict__ partial, int64_t parts,
+                                                     int64_t rows, int64_t cols) {
+  __shared__ float red[2][256 * NV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t rows_per_part = (rows + parts - 1) / parts;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_part, r1 = min(rows, r0 + rows_per_part);
+  float dg[NV][4], db[NV][4], gm[NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t c = ((int64_t)k * 64 + lane) * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dg[k][r] = db[k][r] = 0.f;
+    if (c < cols) ld4<float>(gamma + c, gm[k]);
+    else gm[k][0] = gm[k][1] = gm[k][2] = gm[k][3] = 0.f;
+  }
+  for (int64_t row = r0 + w; row < r1; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NV][4], g[NV][4];
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = ((int64_t)k * 64 + lane) * 4;
+      if (c < cols) {
+        float xv[4], dv[4];
+        ld4<T>(x + row * ldx + c, xv);
+        ld4<T>(dy + row * lddy + c, dv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          xh[k][r] = (xv[r] - mu) * rs;
+          g[k][r] = dv[r] * gm[k][r];
+          sa += g[k][r];
+          sb += g[k][r] * xh[k][r];
+          dg[k][r] += dv[r] * xh[k][r];
+          db[k][r] += dv[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xh[k][r] = g[k][r] = 0.f;
+      }
+    }
+    const float a = wave_sum(sa) / (float)cols;
+    const float b = wave_sum(sb) / (float)cols;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = ((int64_t)k * 64 + lane) * 4;
+      if (c < cols) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = rs * (g[k][r] - a - xh[k][r] * b);
+        if (dres) {
+          float d[4];
+          ld4<T>(dres + row * cols + c, d);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] += d[r];
+        }
+        st4<T>(dx_out + row * cols + c, o);
+        if (drop_out) {
+          const uint32_t base = (uint32_t)(row * cols + c);
+          float dd[4];
+          if (sizeof(T) == 2) {
+            // drop the value as stored (rounded), matching a separate dropout-backward pass over dx_out
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = bf2f(f2bf(o[r]));
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? o[r] * drop_scale : 0.f;
+          st4<T>(drop_out + row * cols + c, dd);
+        }
+      }
+    }
+  }
+  // per-block dgamma/dbeta partial: waves add into LDS in a fixed order (0, 1, 2, 3) -> bitwise reproducible
+  for (int turn = 0; turn < 4; ++turn) {
+    if (w == turn) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cc = (k * 64 + lane) * 4 + r;
+          if (turn == 0) {
+            red[0][cc] = dg[k][r];
+            red[1][cc] = db[k][r];
+          } else {
+            red[0][cc] += dg[k][r];
+            red[1][cc] += db[k][r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int64_t c = threadIdx.x; c < cols; c += 256) {
+    partial[(int64_t)blockIdx.x * cols + c] = red[0][c];
+    partial[(parts + blockIdx.x) * cols + c] = red[1][c];
+  }
+}
+
+template <int NV, class T>
+int ln_fwd_launch(const T* x, int64_t ldx, const float* g, const float* b, T* y, int64_t ldy, float* mean,
+                  float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s) {
+  const unsigned grid = (unsigned)((rows + 3) / 4);
+  ln_fwd_kernel<T, NV><<<grid, 256, 0, s>>>(x, ldx, g, b, y, ldy, mean, rstd, rows, cols, eps);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols) {
+  (void)cols;
+  int64_t p = (rows + 15) / 16;  // >= 16 rows (4 per wave) per block
+  if (p > LN_BWD_PARTS_MAX) p = LN_BWD_PARTS_MAX;
+  if (p < 1) p = 1;
+  return p;
+}
+
+#define NV_SWITCH(cols, CALL)                                           \
+  switch ((int)(((cols) + 255) / 256)) {                                 \
+    case 1: CALL(1); break;                                              \
+    case 2: CALL(2); break;                                              \
+    case 3: CALL(3); break;                                              \
+    case 4: CALL(4); break;                                              \
+    case 5: case 6: CALL(6); break;                                      \
+    case 7: case 8: CALL(8); break;                                      \
+    case 9: case 10: case 11: case 12: CALL(12); break;                  \
+    case 13: case 14: case 15: case 16: CALL(16); break;                 \
+    default: vit::set_error("layernorm: cols=%lld too large", (long long)(cols)); return VIT_ERR_INVALID; \
+  }
+
+extern "C" int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma, const float* beta, void* y,
+                                 int64_t ldy, float* mean, float* rstd, int64_t rows, int64_t cols, float eps,
+                                 int32_t dtype, void* stream) {
+  VIT_REQUIRE(x && gamma && beta && y && mean && rstd && rows > 0 && cols > 0, "vit_layernorm_fwd: bad arguments");
+  VIT_REQUIRE(cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0, "vit_layernorm_fwd: cols/ld must be multiples of 4");
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16) {
+#define CALLB(NV) ln_fwd_launch<NV, bf16_t>((const bf16_t*)x, ldx, gamma, beta, (bf16_t*)y, ldy, mean, rstd, rows, cols, eps, s)
+    NV_SWITCH(cols, CALLB)
+#undef CALLB
+  } else {
+#define CALLF(NV) ln_fwd_launch<NV, float>((const float*)x, ldx, gamma, beta, (float*)y, ldy, mean, rstd, rows, cols, eps, s)
+    NV_SWITCH(cols, CALLF)
+#undef CALLF
+  }
+  return vit::check_launch("vit_layernorm_fwd");
+}
+
+extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
+                                 const float* mean, const float* rstd, const void* dres, void* dx_out,
+                                 void* drop_out, float drop_p, uint32_t drop_seed, float* partial, int64_t rows,
+                                 int64_t cols, int32_t dtype, void* stream) {
+  VIT_REQUIRE(dy && x && gamma && mean && rstd && dx_out && partial && rows > 0 && cols > 0,
+              "vit_layernorm_bwd: bad arguments");
+  VIT_REQUIRE(cols % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0, "vit_layernorm_bwd: cols/ld must be multiples of 4");
+  VIT_REQUIRE(cols <= 4096, "vit_layernorm_bwd: cols=%lld > 4096", (long long)cols);
+  VIT_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "vit_layernorm_bwd: drop_p out of range");
+  const int64_t parts = vit_layernorm_bwd_parts(rows, cols);
+  double t = (double)drop_p * 4294967296.0;
+  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const float scale = 1.0f / (1.0f - drop_p);
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16) {
+#define CALLB(NV)                                                                                               \
+  ln_bwd_kernel<bf16_t, NV><<<(unsigned)parts, 256, 0, s>>>(                                                    \
+      (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
+      (bf16_t*)drop_out, thr, scale, drop_seed, partial, parts, rows, cols)
+    NV_SWITCH(cols, CALLB)
+#undef CALLB
+  } else {
+#define CALLF(NV)                                                                                            \
+  ln_bwd_kernel<float, NV><<<(unsigned)parts, 256, 0, s>>>(                                                  \
+      (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out,   \
+      (float*)drop_out, thr, scale, drop_seed, partial, parts, rows, cols)
+    NV_SWITCH(cols, CALLF)
+#undef CALLF
+  }
+  return vit::check_launch("vit_layernorm_bwd");
+}
