@@ -131,6 +131,8 @@ int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64
                int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
                void* stream);
 int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed, void* stream);
+/* dx = dy * (y > 0): ReLU backward for the module-level FeedForward path (transformer.py:57). */
+int vit_relu_bwd(const void* dy, const void* y, void* dx, int32_t dtype, int64_t n, void* stream);
 int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream);
 int vit_gelu_bwd(const float* x, const float* dy, float* dx, int64_t n, void* stream);
 int vit_softmax_xent(const float* logits, const int64_t* labels, int64_t rows, int64_t classes, float* loss,

@@ -98,15 +98,30 @@ def main():
         opt.step()
         trace.append(float(ls.item()))
     post = {k: float(v.double().norm()) for k, v in m.state_dict().items()}
+    # the same 3 steps in fp64: the spread between the fp32 and fp64 traces is the reference's own sensitivity
+    # (AdamW's first steps are ~lr*sign(g), so ~1e-7 gradient noise flips tiny components)
+    m, _ = ref_model(D, H, L, img, B, nc)
+    m = m.double().eval()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    trace64 = []
+    for _ in range(3):
+        ls = torch.nn.functional.cross_entropy(m(x.double()), y)
+        opt.zero_grad(set_to_none=True)
+        ls.backward()
+        opt.step()
+        trace64.append(float(ls.item()))
     m64, _ = ref_model(D, H, L, img, B, nc)
     m64 = m64.double().eval()
-    with torch.no_grad():
-        logits64 = m64(x.double())
+    logits64 = m64(x.double())
+    torch.nn.functional.cross_entropy(logits64, y).backward()
+    grads64 = {k: p.grad.detach().clone() for k, p in m64.named_parameters()}
+    logits64 = logits64.detach()
     np.savez_compressed(os.path.join(HERE, "tiny.npz"), logits=logits.numpy(), logits64=logits64.numpy(),
-                        loss=loss.numpy(), trace=np.array(trace),
+                        loss=loss.numpy(), trace=np.array(trace), trace64=np.array(trace64),
                         gnorm_keys=np.array(list(gnorm.keys())), gnorm=np.array(list(gnorm.values())),
                         post_keys=np.array(list(post.keys())), post_norm=np.array(list(post.values())),
-                        **{"gslice/" + k: v.reshape(-1)[::97].numpy() for k, v in grads.items()})
+                        **{"gslice/" + k: v.reshape(-1)[::97].numpy() for k, v in grads.items()},
+                        **{"gslice64/" + k: v.reshape(-1)[::97].numpy() for k, v in grads64.items()})
 
     # ---------------- G3: per-op KATs ----------------
     torch.manual_seed(7)

@@ -44,7 +44,7 @@ def test_gemm_bf16_rejects_unaligned_contiguous_dim():
     A = torch.zeros(24, 50, dtype=torch.bfloat16, device=DEV)   # rowstrided A with M = 50 (not a multiple of 8)
     B = torch.zeros(24, 40, dtype=torch.bfloat16, device=DEV)
     C = torch.empty(50, 40, device=DEV)
-    with pytest.raises(RuntimeError, match="multiple of 8"):
+    with pytest.raises(RuntimeError, match="multiple"):
         _ops.gemm(A, B, C, 50, 40, 24, 50, 40, 40, a_kcontig=False, b_kcontig=False)
 
 

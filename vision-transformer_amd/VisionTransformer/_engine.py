@@ -1,0 +1,473 @@
+"""Fused whole-model engine behind `VisionTransformer.forward` (the training hot path).
+
+One autograd node covers the whole network: the forward (vit.py:77-80 -> transformer.py:76-79 per block ->
+vit.py:69-74) runs as a fixed sequence of libvit_hip kernels on the current HIP stream and keeps every activation
+the backward needs resident in HBM (ViT-B/16 at B=256 bf16: ~10 GB of 288 GB); the backward replays the block
+sequence in reverse and writes every parameter gradient straight into ONE flat fp32 gradient buffer whose views are
+exposed as `param.grad`.
+
+Layouts (device):
+  * master weights: the module's own fp32 nn.Parameters, untouched (state_dict/optimizer compatibility with the
+    reference keys, including per-head `heads.{h}.{key,query,value}.weight`);
+  * compute shadow: one buffer in the compute dtype holding, per block, the FUSED QKV matrix [3D, D] (query rows of
+    every head, then keys, then values), proj [D, D], fc1 [4D, D], fc2 [D, 4D], and the patch-embedding matrix
+    [D, C*P*P]; refreshed by the fused AdamW kernel (or a pack kernel after any external write);
+  * gradients: one flat fp32 buffer ordered head | block L-1 | ... | block 0 | embedding, i.e. in the order the
+    backward produces them, so data-parallel all-reduce buckets are contiguous ranges launched as soon as a block's
+    backward is enqueued (RCCL on its own stream, overlapping the remaining backward).
+"""
+from __future__ import annotations
+
+import math
+import weakref
+
+import torch
+import torch.distributed as dist
+
+from . import _ops
+from ._ops import ACT_NONE, ACT_RELU
+
+DROPOUT_P = 0.2          # transformer.py:35,53 (config.dropout is stored but unused by the reference)
+LN_EPS = 1e-5
+ALIGN = 64               # elements; every sub-tensor of the flat buffers starts 256-B aligned
+
+
+def _hash_u32(seed, idx):
+    """Python twin of the device `vit_hash_u32` (murmur3 fmix32 of idx*golden + seed)."""
+    x = (idx * 0x9E3779B1 + seed) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def site_seed(base_seed, layer, site):
+    """Dropout seed of (layer, site); site 0 = MHA output (transformer.py:47), 1 = FFN output (:59)."""
+    return _hash_u32((base_seed * 0x632BE5AB + 0x1234567) & 0xFFFFFFFF, layer * 2 + site)
+
+
+class _Region:
+    def __init__(self):
+        self.size = 0
+        self.items = []
+
+    def add(self, name, numel):
+        off = self.size
+        self.items.append((name, off, numel))
+        self.size = off + ((numel + ALIGN - 1) // ALIGN) * ALIGN
+        return off
+
+
+def split_k_for(m, n, k, kt=64):
+    """K split for a weight-gradient GEMM (reduction over B*T rows): ~1024 workgroups of 128x128 tiles (two per CU,
+    two rounds), each split >= 8 k-tiles deep, at most 32 slabs."""
+    tiles = ((m + 127) // 128) * ((n + 127) // 128)
+    nkt = (k + kt - 1) // kt
+    return max(1, min((1024 + tiles - 1) // tiles, max(1, nkt // 8), 32))
+
+
+class Tape:
+    """Activations saved by a training forward."""
+    __slots__ = ("B", "cols", "blocks", "z", "u", "gz", "zn", "mh", "rh", "seed", "training")
+
+
+class Engine:
+    def __init__(self, model):
+        self.model_ref = weakref.ref(model)
+        cfg = model.vit_config
+        self.C, self.P = cfg.input_channels, cfg.patch_size
+        self.D, self.H, self.L = cfg.embedding_size, cfg.num_heads, cfg.num_blocks
+        self.hd = self.D // self.H
+        self.N = cfg.num_patches
+        self.T = self.N + 1
+        self.nc = cfg.num_classes
+        self.B = cfg.batch_size
+        self.CPP = self.C * self.P * self.P
+        self.dtype = model.compute_dtype
+        self.scale = float(self.hd) ** 0.5          # MULTIPLIED (transformer.py:24)
+        self.device = None
+        self.params = None
+        self.ddp_group = None
+        self.ddp_enabled = False
+        self._works = []
+        self._ws = None
+        self._ptr_sig = None
+        self._ver_sig = None
+        self.stats = {"packs": 0}
+        self.profile_hook = None          # callable(name, phase) around named launches (bench.py HIP events)
+
+    # ------------------------------------------------------------------------------------------------------------
+    # layout
+    # ------------------------------------------------------------------------------------------------------------
+    def _collect(self, model):
+        """name -> Parameter for the fused layout, following the reference module tree."""
+        enc = model.transformer_encoder.blocks
+        emb = model.emdeddings
+        p = {"conv_w": emb.sequence[0].weight, "conv_b": emb.sequence[0].bias,
+             "cls": emb.cls_tkn_embd, "pos": emb.pos_embd,
+             "h0_w": model.mlp[0].weight, "h0_b": model.mlp[0].bias,
+             "hln_w": model.mlp[2].weight, "hln_b": model.mlp[2].bias,
+             "h3_w": model.mlp[3].weight, "h3_b": model.mlp[3].bias}
+        for l, blk in enumerate(enc):
+            mh = blk.multi_head
+            for h, head in enumerate(mh.heads):
+                p[f"{l}.q{h}"] = head.query.weight
+                p[f"{l}.k{h}"] = head.key.weight
+                p[f"{l}.v{h}"] = head.value.weight
+            p[f"{l}.proj_w"], p[f"{l}.proj_b"] = mh.proj.weight, mh.proj.bias
+            p[f"{l}.fc1_w"], p[f"{l}.fc1_b"] = blk.ffwd.mlp[0].weight, blk.ffwd.mlp[0].bias
+            p[f"{l}.fc2_w"], p[f"{l}.fc2_b"] = blk.ffwd.mlp[2].weight, blk.ffwd.mlp[2].bias
+            p[f"{l}.ln1_w"], p[f"{l}.ln1_b"] = blk.ln1.weight, blk.ln1.bias
+            p[f"{l}.ln2_w"], p[f"{l}.ln2_b"] = blk.ln2.weight, blk.ln2.bias
+        return p
+
+    def _build(self, model, device):
+        D, H, hd, L = self.D, self.H, self.hd, self.L
+        params = self._collect(model)
+        for n, t in params.items():
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError(f"parameter {n} must be contiguous float32 master weights (got {t.dtype})")
+            if t.device != device:
+                raise RuntimeError(f"parameter {n} is on {t.device}, expected {device}; call model.to(device)")
+        # ---- gradient layout: head | blocks L-1..0 | embedding
+        g = _Region()
+        goff = {}
+        head_start = g.size
+        for n in ("h0_w", "h0_b", "hln_w", "hln_b", "h3_w", "h3_b"):
+            goff[n] = g.add(n, params[n].numel())
+        self.head_range = (head_start, g.size)
+        self.block_range = {}
+        for l in reversed(range(L)):
+            start = g.size
+            goff[f"{l}.qkv_w"] = g.add(f"{l}.qkv_w", 3 * D * D)
+            for n in ("proj_w", "proj_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b", "ln1_w", "ln1_b", "ln2_w", "ln2_b"):
+                goff[f"{l}.{n}"] = g.add(f"{l}.{n}", params[f"{l}.{n}"].numel())
+            self.block_range[l] = (start, g.size)
+        start = g.size
+        for n in ("conv_w", "conv_b", "cls", "pos"):
+            goff[n] = g.add(n, params[n].numel())
+        self.embed_range = (start, g.size)
+        self.G = torch.zeros(g.size, dtype=torch.float32, device=device)
+        # ---- compute shadow layout
+        s = _Region()
+        soff = {}
+        for l in range(L):
+            soff[f"{l}.qkv_w"] = s.add(f"{l}.qkv_w", 3 * D * D)
+            for n in ("proj_w", "fc1_w", "fc2_w"):
+                soff[f"{l}.{n}"] = s.add(f"{l}.{n}", params[f"{l}.{n}"].numel())
+        soff["conv_w"] = s.add("conv_w", params["conv_w"].numel())
+        self.W = torch.empty(s.size, dtype=self.dtype, device=device)
+
+        def gview(name, shape):
+            o = goff[name]
+            n = math.prod(shape)
+            return self.G[o:o + n].view(shape)
+
+        def wview(name, shape):
+            o = soff[name]
+            n = math.prod(shape)
+            return self.W[o:o + n].view(shape)
+
+        # fused compute/grad views
+        self.gw, self.ww = {}, {}
+        for l in range(L):
+            self.gw[f"{l}.qkv_w"] = gview(f"{l}.qkv_w", (3 * D, D))
+            self.ww[f"{l}.qkv_w"] = wview(f"{l}.qkv_w", (3 * D, D))
+            for n in ("proj_w", "fc1_w", "fc2_w"):
+                shp = tuple(params[f"{l}.{n}"].shape)
+                self.gw[f"{l}.{n}"] = gview(f"{l}.{n}", shp)
+                self.ww[f"{l}.{n}"] = wview(f"{l}.{n}", shp)
+            for n in ("proj_b", "fc1_b", "fc2_b", "ln1_w", "ln1_b", "ln2_w", "ln2_b"):
+                self.gw[f"{l}.{n}"] = gview(f"{l}.{n}", tuple(params[f"{l}.{n}"].shape))
+        for n in ("h0_w", "h0_b", "hln_w", "hln_b", "h3_w", "h3_b", "conv_b", "cls", "pos"):
+            self.gw[n] = gview(n, tuple(params[n].shape))
+        self.gw["conv_w"] = gview("conv_w", (D, self.CPP))
+        self.ww["conv_w"] = wview("conv_w", (D, self.CPP))
+
+        # per-parameter grad view + shadow view (the optimizer refreshes the shadow in its kernel)
+        self.grad_views = []
+        self.pack_entries = []
+        for name, p in params.items():
+            l, _, short = name.partition(".") if "." in name else ("", "", name)
+            if short and short[0] in "qkv" and short[1:].isdigit():
+                h = int(short[1:])
+                row0 = {"q": 0, "k": D, "v": 2 * D}[short[0]] + h * hd
+                gv = self.gw[f"{l}.qkv_w"][row0:row0 + hd]
+                sv = self.ww[f"{l}.qkv_w"][row0:row0 + hd]
+            else:
+                key = name
+                gv = self.gw[key].view(p.shape)
+                sv = self.ww[key].view(p.shape) if key in self.ww else None
+            self.grad_views.append((p, gv))
+            p._vit_shadow = sv
+            p._vit_engine = weakref.ref(self)
+            if sv is not None:
+                self.pack_entries.append((p, sv))
+        self.params = params
+        self.param_list = list(params.values())
+        self.device = device
+        self._pack_table = None
+        self._ptr_sig = self._pointer_signature()
+        self._ver_sig = None
+
+    def _pointer_signature(self):
+        return tuple(p.data_ptr() for p in self.param_list)
+
+    def _version_signature(self):
+        return sum(p._version for p in self.param_list)
+
+    def ensure_ready(self, device):
+        model = self.model_ref()
+        if self.params is None or self.device != device or self._pointer_signature() != self._ptr_sig:
+            self._build(model, device)
+        ver = self._version_signature()
+        if ver != self._ver_sig:
+            self.repack()
+            self._ver_sig = ver
+
+    def repack(self):
+        """shadow <- compute-dtype copy of the fp32 master matrices (one multi-tensor launch)."""
+        if self._pack_table is None:
+            entries = [(p.detach(), None, None, None, sv) for p, sv in self.pack_entries]
+            self._pack_table = _ops.build_chunk_table(entries, self.device)
+        tab, n = self._pack_table
+        _ops.pack(tab, n, self.dtype)
+        self.stats["packs"] += 1
+
+    def mark_shadow_fresh(self):
+        self._ver_sig = self._version_signature()
+
+    # ------------------------------------------------------------------------------------------------------------
+    def _workspace(self, nbytes):
+        if self._ws is None or self._ws.numel() * 4 < nbytes:
+            self._ws = torch.empty(max(nbytes // 4 + 1, 1 << 20), dtype=torch.float32, device=self.device)
+        return self._ws
+
+    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta):
+        """out[m][n] (+)= sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K."""
+        split = split_k_for(m, n, k)
+        need = split * m * n * 4 if split > 1 else 0
+        ws = self._workspace(need) if split > 1 else None
+        _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
+                  split_k=split, workspace=ws)
+
+    def _colsum(self, x, rows, cols, ld, out, beta):
+        _ops.colsum(x, rows, cols, ld, out, beta=beta)
+
+    def _attach_grads(self):
+        """Expose the flat gradient buffer as param.grad; returns beta (1.0 accumulate / 0.0 overwrite)."""
+        live = [p.grad is not None and p.grad.data_ptr() == gv.data_ptr() for p, gv in self.grad_views]
+        if all(live):
+            return 1.0
+        if not any(p.grad is not None for p, _ in self.grad_views):
+            for p, gv in self.grad_views:
+                p.grad = gv
+            return 0.0
+        # mixed: zero the regions whose grad was dropped/replaced, keep accumulating elsewhere
+        for (p, gv), ok in zip(self.grad_views, live):
+            if not ok:
+                if p.grad is not None:
+                    gv.copy_(p.grad)
+                else:
+                    gv.zero_()
+                p.grad = gv
+        return 1.0
+
+    # ------------------------------------------------------------------------------------------------------------
+    # forward
+    # ------------------------------------------------------------------------------------------------------------
+    def forward(self, x, training, save, want_probs=False):
+        model = self.model_ref()
+        if not x.is_cuda:
+            raise RuntimeError("VisionTransformer (HIP path) needs the input on a ROCm device; there is no CPU path")
+        if x.dim() != 4 or x.shape[1] != self.C or x.shape[2] % self.P or x.shape[3] % self.P:
+            raise RuntimeError(f"expected input [B, {self.C}, H, W] with H, W multiples of {self.P}, got "
+                               f"{tuple(x.shape)}")
+        B = x.shape[0]
+        self.ensure_ready(x.device)
+        if (x.shape[2] // self.P) * (x.shape[3] // self.P) != self.N:
+            raise RuntimeError(f"image gives {(x.shape[2] // self.P) * (x.shape[3] // self.P)} patches but "
+                               f"config.num_patches = {self.N} (pos_embd has {self.T} rows)")
+        if B != self.params["cls"].shape[0]:
+            # the reference concatenates a batch-shaped CLS parameter (vit.py:32,41) and fails the same way
+            raise RuntimeError(f"batch size {B} != config.batch_size {self.params['cls'].shape[0]} "
+                               "(the CLS token parameter is batch-shaped)")
+        x = x.contiguous()
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        D, T, N, H, hd, L, dt = self.D, self.T, self.N, self.H, self.hd, self.L, self.dtype
+        M = B * T
+        prm = self.params
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training else 0
+        tape = Tape() if save else None
+
+        cols = _ops.im2col(x, self.P, dt)                                             # vit.py:21-29 as GEMM
+        xcur = torch.empty(M, D, dtype=dt, device=x.device)
+        _ops.gemm(cols, self.ww["conv_w"], xcur, B * N, D, self.CPP, self.CPP, self.CPP, D, bias=prm["conv_b"],
+                  res=prm["pos"].view(T, D), ldres=D, res_rowmod=N, out_group=(N, T))  # + pos, rows -> b*T+n
+        _ops.embed_cls(prm["cls"], prm["pos"], xcur, B, T, D)                           # CLS appended LAST (vit.py:41)
+        blocks = []
+        for l in range(L):
+            blk = model.transformer_encoder.blocks[l]
+            x_in = xcur
+            a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
+            qkv = _ops.linear(a1, self.ww[f"{l}.qkv_w"])                                # 3H heads' K/Q/V in one GEMM
+            probs = None
+            if want_probs:
+                probs = torch.empty(B, H, T, T, dtype=torch.float32, device=x.device)
+            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs)
+            blk.multi_head.attention_probs = probs
+            x_mid = torch.empty(M, D, dtype=dt, device=x.device)
+            _ops.gemm(o, self.ww[f"{l}.proj_w"], x_mid, M, D, D, D, D, D, bias=prm[f"{l}.proj_b"], res=x_in,
+                      ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 0))
+            a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
+            hook = self.profile_hook
+            if hook:
+                hook("fc1_fwd", 0)
+            h = _ops.linear(a2, self.ww[f"{l}.fc1_w"], bias=prm[f"{l}.fc1_b"], act=ACT_RELU)
+            if hook:
+                hook("fc1_fwd", 1)
+            x_out = torch.empty(M, D, dtype=dt, device=x.device)
+            _ops.gemm(h, self.ww[f"{l}.fc2_w"], x_out, M, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
+                      res=x_mid, ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 1))
+            if save:
+                blocks.append((x_in, a1, m1, r1, qkv, o, lse, x_mid, a2, m2, r2, h))
+            xcur = x_out
+        # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
+        z = torch.empty(B, D, dtype=torch.float32, device=x.device)
+        _ops.copy2d(xcur, T * D, z, D, B, D)
+        u = _ops.linear(z, prm["h0_w"], bias=prm["h0_b"])
+        gz = _ops.gelu_fwd(u)
+        zn, mh, rh = _ops.layernorm_fwd(gz, prm["hln_w"], prm["hln_b"], eps=LN_EPS)
+        logits = _ops.linear(zn, prm["h3_w"], bias=prm["h3_b"])
+        if save:
+            tape.B, tape.cols, tape.blocks = B, cols, blocks
+            tape.z, tape.u, tape.gz, tape.zn, tape.mh, tape.rh = z, u, gz, zn, mh, rh
+            tape.seed, tape.training = seed, training
+        return logits, tape
+
+    # ------------------------------------------------------------------------------------------------------------
+    # backward
+    # ------------------------------------------------------------------------------------------------------------
+    def _bucket_ready(self, rng):
+        """Launch the all-reduce of one contiguous gradient range (RCCL stream waits on the compute stream)."""
+        if self.ddp_enabled:
+            a, b = rng
+            if dist.get_backend(self.ddp_group) == "nccl":      # RCCL: native average
+                w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
+                self._works.append((w, None))
+            else:                                             # gloo (CPU tests): sum, scaled after the wait
+                w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.SUM, group=self.ddp_group, async_op=True)
+                self._works.append((w, (a, b)))
+
+    def _finish_buckets(self):
+        world = dist.get_world_size(self.ddp_group) if self.ddp_enabled else 1
+        for w, rng in self._works:
+            w.wait()
+            if rng is not None:
+                self.G[rng[0]:rng[1]].mul_(1.0 / world)
+        self._works = []
+
+    def backward(self, tape, dlogits):
+        D, T, N, H, hd, L, dt = self.D, self.T, self.N, self.H, self.hd, self.L, self.dtype
+        B = tape.B
+        M = B * T
+        prm, gw = self.params, self.gw
+        # decided at backward time: the reference calls zero_grad(set_to_none=True) between forward and backward
+        beta = self._attach_grads()
+        dev = dlogits.device
+        dlogits = dlogits.contiguous().float()
+        nc = self.nc
+        # ---- head (fp32)
+        dzn = torch.empty(B, 4 * D, dtype=torch.float32, device=dev)
+        _ops.gemm(dlogits, prm["h3_w"], dzn, B, 4 * D, nc, nc, 4 * D, 4 * D, b_kcontig=False)
+        self._wgrad(dlogits, tape.zn, gw["h3_w"], nc, 4 * D, B, nc, 4 * D, beta)
+        self._colsum(dlogits, B, nc, nc, gw["h3_b"], beta)
+        dgz = torch.empty_like(tape.gz)
+        part = _ops.layernorm_bwd(dzn, tape.gz, prm["hln_w"], tape.mh, tape.rh, dgz)
+        self._colsum(part[0], part.shape[1], 4 * D, 4 * D, gw["hln_w"], beta)
+        self._colsum(part[1], part.shape[1], 4 * D, 4 * D, gw["hln_b"], beta)
+        du = _ops.gelu_bwd(tape.u, dgz)
+        dz = torch.empty(B, D, dtype=torch.float32, device=dev)
+        _ops.gemm(du, prm["h0_w"], dz, B, D, 4 * D, 4 * D, D, D, b_kcontig=False)
+        self._wgrad(du, tape.z, gw["h0_w"], 4 * D, D, B, 4 * D, D, beta)
+        self._colsum(du, B, 4 * D, 4 * D, gw["h0_b"], beta)
+        self._bucket_ready(self.head_range)
+        # ---- d(encoder output): only token-0 rows are nonzero
+        dx = torch.zeros(M, D, dtype=dt, device=dev)
+        _ops.copy2d(dz, D, dx, T * D, B, D)
+        g1 = torch.empty_like(dx)
+        if tape.training:
+            _ops.dropout_bwd(dx, g1, DROPOUT_P, site_seed(tape.seed, L - 1, 1))
+        else:
+            g1 = dx
+        for l in reversed(range(L)):
+            x_in, a1, m1, r1, qkv, o, lse, x_mid, a2, m2, r2, h = tape.blocks[l]
+            # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
+            dh = torch.empty(M, 4 * D, dtype=dt, device=dev)
+            _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=h,
+                      ldaux=4 * D)                                                        # relu backward fused
+            self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta)
+            self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta)
+            da2 = torch.empty(M, D, dtype=dt, device=dev)
+            _ops.gemm(dh, self.ww[f"{l}.fc1_w"], da2, M, D, 4 * D, 4 * D, D, D, b_kcontig=False)
+            self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, M, 4 * D, D, beta)
+            self._colsum(dh, M, 4 * D, 4 * D, gw[f"{l}.fc1_b"], beta)
+            dx_mid = torch.empty(M, D, dtype=dt, device=dev)
+            g0 = torch.empty(M, D, dtype=dt, device=dev) if tape.training else None
+            part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx,
+                                      drop_out=g0, drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l, 0))
+            self._colsum(part[0], part.shape[1], D, D, gw[f"{l}.ln2_w"], beta)
+            self._colsum(part[1], part.shape[1], D, D, gw[f"{l}.ln2_b"], beta)
+            if g0 is None:
+                g0 = dx_mid
+            # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
+            do = torch.empty(M, D, dtype=dt, device=dev)
+            _ops.gemm(g0, self.ww[f"{l}.proj_w"], do, M, D, D, D, D, D, b_kcontig=False)
+            self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta)
+            self._colsum(g0, M, D, D, gw[f"{l}.proj_b"], beta)
+            dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
+                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)))
+            da1 = torch.empty(M, D, dtype=dt, device=dev)
+            _ops.gemm(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
+            self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta)
+            dx_in = torch.empty(M, D, dtype=dt, device=dev)
+            g1n = torch.empty(M, D, dtype=dt, device=dev) if (tape.training and l > 0) else None
+            part = _ops.layernorm_bwd(da1, x_in, prm[f"{l}.ln1_w"], m1, r1, dx_in, dres=dx_mid, drop_out=g1n,
+                                      drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l - 1, 1) if l > 0 else 0)
+            self._colsum(part[0], part.shape[1], D, D, gw[f"{l}.ln1_w"], beta)
+            self._colsum(part[1], part.shape[1], D, D, gw[f"{l}.ln1_b"], beta)
+            self._bucket_ready(self.block_range[l])
+            dx = dx_in
+            g1 = g1n if g1n is not None else dx_in
+        # ---- embedding (vit.py:39-42): dx = d(x0) [B*T, D]
+        _ops.copy2d(dx[N:], T * D, gw["cls"].view(B, D), D, B, D, beta=beta)           # CLS row of every image
+        self._colsum(dx, B, T * D, T * D, gw["pos"].view(-1), beta)                     # pos: sum over the batch
+        dpatch = torch.empty(B * N, D, dtype=dt, device=dev)
+        _ops.copy2d(dx, D, dpatch, D, B * N, D, group=(N, T))
+        self._colsum(dpatch, B * N, D, D, gw["conv_b"], beta)
+        self._wgrad(dpatch, tape.cols, gw["conv_w"], D, self.CPP, B * N, D, self.CPP, beta)
+        self._bucket_ready(self.embed_range)
+        if self._works:
+            self._finish_buckets()
+
+
+class ViTFunction(torch.autograd.Function):
+    """One autograd node for the whole network; gradients land in the engine's flat buffer (param.grad views)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, engine, training, want_probs):
+        logits, tape = engine.forward(x, training, save=True, want_probs=want_probs)
+        ctx.engine = engine
+        ctx.tape = tape
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        if ctx.tape is None:
+            raise RuntimeError("VisionTransformer backward called twice on the same forward")
+        ctx.engine.backward(ctx.tape, dlogits)
+        ctx.tape = None
+        return None, None, None, None, None

@@ -161,6 +161,12 @@ def dropout_bwd(x, y, p, seed, stream=None):
     return y
 
 
+def relu_bwd(dy, y, dx=None, stream=None):
+    dx = torch.empty_like(dy) if dx is None else dx
+    _lib.call("vit_relu_bwd", _ptr(dy), _ptr(y), _ptr(dx), dtype_code(dy), dy.numel(), _stream(stream))
+    return dx
+
+
 def gelu_fwd(x, y=None, stream=None):
     y = torch.empty_like(x) if y is None else y
     _lib.call("vit_gelu_fwd", _ptr(x), _ptr(y), x.numel(), _stream(stream))

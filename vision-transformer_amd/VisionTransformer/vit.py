@@ -1,0 +1,103 @@
+"""PatchEmbedding and VisionTransformer — drop-in for src/VisionTransformer/vit.py.
+
+Same constructors, attribute names (including the reference's `emdeddings` spelling), parameters, state_dict keys and
+init draw order as the reference (vit.py:9-80).  `VisionTransformer.forward` runs the fused MI355X engine
+(`_engine.Engine`): patch im2col + MFMA GEMM with bias/pos epilogue, L encoder blocks of fused kernels, and the
+classifier MLP on token 0 (the first PATCH token, because the CLS token is appended last — vit.py:41,80).
+
+Extra (additive) API:
+  * `model.compute_dtype` — from ViTConfig (bf16 or fp32 arithmetic);
+  * `model.store_attention_probs = True` — fill each block's `multi_head.attention_probs` [B, H, T, T] during the
+    fused forward (the reference always materialises it, transformer.py:48; here it is opt-in because it is 477 MB
+    per layer at ViT-B/16, B=256);
+  * `model.enable_data_parallel(group=None)` — all-reduce (average) gradients over `torch.distributed` (RCCL)
+    bucket-by-bucket while the backward is still running;
+  * `model.hip_engine` — the engine (flat gradient / shadow-weight buffers).
+"""
+import torch
+import torch.nn as nn
+
+from . import _functional as Fh
+from . import config as _config  # noqa: F401  (reference module imports config alongside transformer)
+from . import transformer
+from ._engine import Engine, ViTFunction
+
+
+class PatchEmbedding(nn.Module):
+    def __init__(self, input_channels, embedding_size, patch_size, batch_size, num_patches, precision, device):
+        super().__init__()
+        # master weights are fp32 regardless of `precision` (which selects the compute dtype instead)
+        self.sequence = nn.Sequential(
+            nn.Conv2d(in_channels=input_channels, out_channels=embedding_size, kernel_size=patch_size,
+                      stride=patch_size, device=device, dtype=torch.float32),
+            nn.Flatten(2),
+        )
+        self.cls_tkn_embd = nn.Parameter(torch.randn(size=(batch_size, 1, embedding_size), device=device),
+                                         requires_grad=True)
+        self.pos_embd = nn.Parameter(torch.randn(size=(1, num_patches + 1, embedding_size), device=device),
+                                     requires_grad=True)
+        self.patch_size = patch_size
+        self.compute_dtype = precision if precision in (torch.float32, torch.bfloat16) else torch.float32
+
+    def forward(self, x):
+        conv = self.sequence[0]
+        return Fh.PatchEmbedFn.apply(x, conv.weight, conv.bias, self.cls_tkn_embd, self.pos_embd, self.patch_size,
+                                     self.compute_dtype)
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, config):
+        super().__init__()
+        self.vit_config = config
+        self.compute_dtype = getattr(config, "compute_dtype", None) or (
+            config.precision if config.precision in (torch.float32, torch.bfloat16) else torch.float32)
+        self.emdeddings = PatchEmbedding(
+            input_channels=config.input_channels,
+            embedding_size=config.embedding_size,
+            patch_size=config.patch_size,
+            num_patches=config.num_patches,
+            precision=self.compute_dtype,
+            batch_size=config.batch_size,
+            device=config.device,
+        )
+        self.transformer_encoder = transformer.TransformerEncoder(
+            embedding_size=config.embedding_size,
+            num_heads=config.num_heads,
+            num_blocks=config.num_blocks,
+            block_size=config.num_patches + 1,
+        )
+        self.mlp = nn.Sequential(
+            nn.Linear(config.embedding_size, 4 * config.embedding_size),
+            nn.GELU(),
+            nn.LayerNorm(4 * config.embedding_size),
+            nn.Linear(4 * config.embedding_size, config.num_classes),
+        )
+        self.store_attention_probs = False
+        self._engine = None
+        self._anchor = None
+
+    @property
+    def hip_engine(self):
+        if self._engine is None:
+            self._engine = Engine(self)
+        return self._engine
+
+    def enable_data_parallel(self, group=None):
+        """Average gradients across the process group with RCCL, bucketed per block, overlapped with backward."""
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            raise RuntimeError("enable_data_parallel: torch.distributed is not initialised")
+        eng = self.hip_engine
+        eng.ddp_group = group
+        eng.ddp_enabled = dist.get_world_size(group) > 1
+        return self
+
+    def forward(self, x):
+        eng = self.hip_engine
+        want_grad = torch.is_grad_enabled() and any(p.requires_grad for p in (self.mlp[3].weight,))
+        if want_grad:
+            if self._anchor is None or self._anchor.device != x.device:
+                self._anchor = torch.zeros((), device=x.device, requires_grad=True)
+            return ViTFunction.apply(x, self._anchor, eng, self.training, self.store_attention_probs)
+        logits, _ = eng.forward(x, self.training, save=False, want_probs=self.store_attention_probs)
+        return logits

@@ -12,6 +12,8 @@
 // f32 path: 64x64x16 tile, v_mfma_f32_32x32x2_f32 (bit-for-bit an fp32 fma chain) — exact-fp32 parity path.
 // Split-K (wgrad: reduction over B*T rows): fp32 slabs per K-slice, then a deterministic reduce that applies the
 // same epilogue.
+#include <stdlib.h>
+
 #include "vit_common.h"
 
 namespace {
@@ -280,6 +282,344 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g, EpiParams
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// bf16 MFMA kernel v2: LDS-DMA staging (buffer_load ... lds), XCD-aware tile order, 2-phase pipeline.
+//   Same 128x128x64 tile, wave layout, LDS images and fragment reads as v1.  Each wave issues 4 LDS-DMA
+//   instructions per operand per k-tile (1 KiB each, lane-linear destination); the XOR swizzle of the LDS image is
+//   applied to the per-lane SOURCE address (the destination of an LDS-DMA is base + 16*lane).  Lanes whose source
+//   lies outside the matrix get an out-of-range buffer offset, so the hardware range check writes zeros: every
+//   M/N/K tail is handled without branches.  Loop: issue tile t+1 -> fragments + MFMAs on tile t -> vmcnt(0) +
+//   barrier (one barrier per k-tile).
+// ------------------------------------------------------------------------------------------------------------
+constexpr uint32_t OOB = 0x80000000u;
+
+VIT_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+  const uint32_t nrec = bytes >= 0x7fffffffLL ? 0x7fffffffu : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, 0x00020000);
+}
+
+// Per-lane byte offsets of the 4 LDS-DMA pieces one wave issues per operand per k-tile, at k-tile 0 of the
+// workgroup's K range.  Invalid rows get an out-of-range offset (stays out of range after adding the k offset,
+// because every operand is < 2 GiB), so the buffer range check zero-fills them.
+template <bool KC>
+VIT_DEV void dma_offsets(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int wave, int lane, uint32_t (&off)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ii = wave * 4 + i;
+    int64_t gr, gk;
+    if (KC) {
+      const int r = ii * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      gr = r0 + r;
+      gk = k0 + c * 8;
+    } else {
+      const int kr = ii * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ swz_rs(kr);
+      gk = k0 + kr;
+      gr = r0 + c * 8;
+    }
+    const int64_t eoff = KC ? gr * ld + gk : gk * ld + gr;
+    off[i] = gr < rows ? (uint32_t)(eoff * 2) : OOB;
+  }
+}
+
+VIT_DEV void dma_issue(__amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[4], uint32_t soff, bf16_t* lds_tile,
+                       int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(lds_tile + (wave * 4 + i) * 512), 16, off[i], soff, 0, 0);
+}
+
+template <bool AKC, bool BKC>
+VIT_DEV void read_frags(const bf16_t* As, const bf16_t* Bs, int wm, int wn, int kk, int lane, bf16x8_t (&af)[4],
+                        bf16x8_t (&bfr)[4]) {
+#pragma unroll
+  for (int x = 0; x < 4; ++x) af[x] = read_frag<AKC>(As, wm * 64 + x * 16, kk, lane);
+#pragma unroll
+  for (int y = 0; y < 4; ++y) bfr[y] = read_frag<BKC>(Bs, wn * 64 + y * 16, kk, lane);
+}
+
+// 16 MFMAs on (af, bfr) with the NEXT fragments' LDS reads (into naf, nbf) issued in the MFMA gaps: the reads in
+// flight are always younger than the operands the MFMAs wait for, so hipcc's waits are exact and no LDS-read latency
+// is exposed.
+template <bool AKC, bool BKC>
+VIT_DEV void mfma_4x4_prefetch(f32x4 (&acc)[4][4], const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4],
+                               const bf16_t* As, const bf16_t* Bs, int wm, int wn, int kk, int lane,
+                               bf16x8_t (&naf)[4], bf16x8_t (&nbf)[4]) {
+  constexpr int RA = AKC ? 1 : 2, RB = BKC ? 1 : 2;       // LDS instructions per fragment
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[y], af[x], acc[x][y], 0, 0, 0);
+      const int idx = x * 4 + y;
+      if (idx < 4) nbf[idx] = read_frag<BKC>(Bs, wn * 64 + idx * 16, kk, lane);
+      else if (idx < 8) naf[idx - 4] = read_frag<AKC>(As, wm * 64 + (idx - 4) * 16, kk, lane);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  // pin the interleave: (1 MFMA, one fragment's reads) x 8, then the remaining 8 MFMAs
+#define VIT_PIN(R)                                   \
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); \
+  __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+  VIT_PIN(RB) VIT_PIN(RB) VIT_PIN(RB) VIT_PIN(RB)
+  VIT_PIN(RA) VIT_PIN(RA) VIT_PIN(RA) VIT_PIN(RA)
+#undef VIT_PIN
+  __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+}
+
+// Loop schedule per k-tile kt (tile kt in LDS slot c, fragments of its first 32-deep half already in registers):
+//   read second-half fragments of slot c | MFMAs on the first half | lgkmcnt(0) + vmcnt(0) + barrier (tile kt+1 in
+//   slot c^1; every wave done reading slot c) | LDS-DMA of tile kt+2 into slot c | read first-half fragments of
+//   slot c^1 | MFMAs on the second half.   LDS-read latency hides under MFMAs; each DMA has one full k-tile of lead.
+template <bool AKC, bool BKC, class TO>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_v2(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware bijective remap: workgroups that share an XCD (same blockIdx % 8) get a contiguous range of tiles,
+  // so neighbouring tiles (same A row panel) hit that XCD's L2.
+  const int64_t nwg = gridDim.x, orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int64_t i0 = tm * BM, j0 = tn * BN;
+  const int64_t nkt = g.K / BK;                       // host guarantees K % 64 == 0 for this kernel
+  const int64_t kt0 = (int64_t)blockIdx.y * g.kt_per_split;
+  const int nk = (int)(min(nkt, kt0 + g.kt_per_split) - kt0);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
+  // k-tile strides in bytes (scalar): along the row for k-contiguous operands, along rows for row-strided ones
+  const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
+  const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
+  uint32_t oa[4], ob[4];
+  dma_offsets<AKC>(g.lda, g.M, i0, kt0 * BK, wave, lane, oa);
+  dma_offsets<BKC>(g.ldb, g.N, j0, kt0 * BK, wave, lane, ob);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t a0[4], b0[4], a1[4], b1[4];
+  if (nk > 0) {
+    dma_issue(ra, oa, 0, smem, wave);
+    dma_issue(rb, ob, 0, smem + TILE_ELEMS, wave);
+  }
+  if (nk > 1) {
+    dma_issue(ra, oa, sa, smem + 2 * TILE_ELEMS, wave);
+    dma_issue(rb, ob, sb, smem + 3 * TILE_ELEMS, wave);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed, tile 1 (8 pieces) still in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  read_frags<AKC, BKC>(smem, smem + TILE_ELEMS, wm, wn, 0, lane, a0, b0);
+  uint32_t soa = 2 * sa, sob = 2 * sb;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int c = kt & 1;
+    const bf16_t* As = smem + c * 2 * TILE_ELEMS;
+    const bf16_t* An = smem + (c ^ 1) * 2 * TILE_ELEMS;
+    mfma_4x4_prefetch<AKC, BKC>(acc, a0, b0, As, As + TILE_ELEMS, wm, wn, 1, lane, a1, b1);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) {
+      dma_issue(ra, oa, soa, smem + c * 2 * TILE_ELEMS, wave);
+      dma_issue(rb, ob, sob, smem + c * 2 * TILE_ELEMS + TILE_ELEMS, wave);
+    }
+    soa += sa;
+    sob += sb;
+    // next tile's first-half fragments (a stale slot on the last k-tile: harmless, keeps the reads unconditional)
+    mfma_4x4_prefetch<AKC, BKC>(acc, a1, b1, An, An + TILE_ELEMS, wm, wn, 0, lane, a0, b0);
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int64_t i = i0 + wm * 64 + x * 16 + (lane & 15);
+      const int64_t j = j0 + wn * 64 + y * 16 + 4 * (lane >> 4);
+      float v[4] = {acc[x][y][0], acc[x][y][1], acc[x][y][2], acc[x][y][3]};
+#ifdef VIT_GEMM_NOEPI
+      if (v[0] != 1234.5f) continue;   // diagnostic build: no stores (acc stays live)
+#endif
+      if (g.ws) slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
+      else epilogue4<TO>(e, i, j, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// bf16 MFMA kernel v3: 256 x BN x 64 workgroup tile (BN = 256 or 128), 8 waves (512 threads), LDS-DMA staging
+// with hoisted per-lane offsets, 2 LDS stages (BN=256: 128 KiB -> one workgroup per CU, two waves per SIMD).
+//   Bytes staged per FLOP: 1/2 (BN=256) or 2/3 (BN=128) of the 128x128 tile's — the operand stream per CU, not the
+//   MFMA rate, is what limits the smaller tile.
+//   Wave grid: BN=256 -> 2 (M) x 4 (N) waves of 128x64; BN=128 -> 4 x 2 waves of 64x64.
+//   LDS images: k-contiguous operand [R rows][64 k] (128-B rows, chunk ^ (row & 7)); row-strided operand
+//   [64 k][R] (2R-B rows, chunk ^ swz_rs(k) on the low 4 chunk bits) — the same conflict analysis as v1 since every
+//   row starts on bank 0.
+// ------------------------------------------------------------------------------------------------------------
+template <bool KC, int R>
+VIT_DEV void dma_offsets3(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int wave, int lane, uint32_t* off) {
+  constexpr int NP = R / 64;                 // pieces per wave: (R*64*2 B) / 1 KiB / 8 waves
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int ii = wave * NP + i;
+    int64_t gr, gk;
+    if (KC) {
+      const int r = ii * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      gr = r0 + r;
+      gk = k0 + c * 8;
+    } else {
+      constexpr int RPP = 1024 / (2 * R);    // k-rows per piece
+      constexpr int CPR = R / 8;             // 16-B chunks per k-row
+      const int kr = ii * RPP + lane / CPR;
+      const int c = (lane % CPR) ^ swz_rs(kr);
+      gk = k0 + kr;
+      gr = r0 + c * 8;
+    }
+    const int64_t eoff = KC ? gr * ld + gk : gk * ld + gr;
+    off[i] = gr < rows ? (uint32_t)(eoff * 2) : OOB;
+  }
+}
+
+template <int NP>
+VIT_DEV void dma_issue3(__amdgpu_buffer_rsrc_t rs, const uint32_t* off, uint32_t soff, bf16_t* lds_tile, int wave) {
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(lds_tile + (wave * NP + i) * 512), 16, off[i], soff, 0, 0);
+}
+
+// fragment of 16 rows starting at rb0 (k-step kk) from an R-row image
+template <bool KC, int R>
+VIT_DEV bf16x8_t read_frag3(const bf16_t* lds, int rb0, int kk, int lane) {
+  if (KC) {
+    const int r = rb0 + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    s16x8 v = *reinterpret_cast<const s16x8*>(lds + r * BK + ((c ^ (r & 7)) << 3));
+    return __builtin_bit_cast(bf16x8_t, v);
+  } else {
+    const int lg = lane & 15, q = lg >> 2, p = lg & 3, g = lane >> 4;
+    const int kr = kk * 32 + 8 * g + q;
+    const int c = (rb0 + 4 * p) >> 3;
+    const int sw = swz_rs(kr);
+    s16x4 lo = tr_read(lds + kr * R + ((c ^ sw) << 3) + (p & 1) * 4);
+    s16x4 hi = tr_read(lds + (kr + 4) * R + ((c ^ sw) << 3) + (p & 1) * 4);
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+template <int N>
+VIT_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool AKC, bool BKC, int BN3, class TO>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_v3(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
+  constexpr int BM3 = 256;
+  constexpr int NSTAGE = BN3 == 128 ? 3 : 2;              // LDS ring depth (3 x 48 KiB / 2 x 64 KiB)
+  constexpr int WN = BN3 == 256 ? 4 : 2, WM = 8 / WN;     // wave grid
+  constexpr int TWM = BM3 / WM, TWN = BN3 / WN;           // wave tile
+  constexpr int MX = TWM / 16, NY = TWN / 16;              // 16x16 fragments per wave
+  constexpr int NPA = BM3 / 64, NPB = BN3 / 64;            // LDS-DMA pieces per wave per k-tile
+  constexpr int NPT = NPA + NPB;
+  constexpr int A_ELEMS = BM3 * BK, B_ELEMS = BN3 * BK, STAGE = A_ELEMS + B_ELEMS;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem3[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t nwg = gridDim.x, orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  const int64_t i0 = tm * BM3, j0 = tn * BN3;
+  const int64_t nkt = g.K / BK;
+  const int64_t kt0 = (int64_t)blockIdx.y * g.kt_per_split;
+  const int nk = (int)(min(nkt, kt0 + g.kt_per_split) - kt0);
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
+  const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
+  const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
+  uint32_t oa[NPA], ob[NPB];
+  dma_offsets3<AKC, BM3>(g.lda, g.M, i0, kt0 * BK, wave, lane, oa);
+  dma_offsets3<BKC, BN3>(g.ldb, g.N, j0, kt0 * BK, wave, lane, ob);
+
+  f32x4 acc[MX][NY];
+#pragma unroll
+  for (int x = 0; x < MX; ++x)
+#pragma unroll
+    for (int y = 0; y < NY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: k-tiles 0 .. NSTAGE-2 in flight
+  uint32_t soa = 0, sob = 0;
+#pragma unroll
+  for (int st = 0; st < NSTAGE - 1; ++st) {
+    if (st < nk) {
+      dma_issue3<NPA>(ra, oa, soa, smem3 + st * STAGE, wave);
+      dma_issue3<NPB>(rb, ob, sob, smem3 + st * STAGE + A_ELEMS, wave);
+    }
+    soa += sa;
+    sob += sb;
+  }
+  int rd = 0, wr = NSTAGE - 1;                             // ring slots: read (k-tile kt), write (k-tile kt+NSTAGE-1)
+  for (int kt = 0; kt < nk; ++kt) {
+    // k-tile kt landed for this wave: leave the younger NSTAGE-2 tiles' pieces in flight (counted, never 0 in the
+    // steady state), then a raw barrier (no vmcnt(0) drain) makes every wave's pieces visible.
+    if (NSTAGE == 3 && kt + 1 < nk) wait_vmcnt<NPT>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // refill the slot read in iteration kt-1 (every wave is past that iteration's reads: the barrier above)
+    if (kt + NSTAGE - 1 < nk) {
+      dma_issue3<NPA>(ra, oa, soa, smem3 + wr * STAGE, wave);
+      dma_issue3<NPB>(rb, ob, sob, smem3 + wr * STAGE + A_ELEMS, wave);
+    }
+    soa += sa;
+    sob += sb;
+    const bf16_t* As = smem3 + rd * STAGE;
+    const bf16_t* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t bfr[NY];
+#pragma unroll
+      for (int y = 0; y < NY; ++y) bfr[y] = read_frag3<BKC, BN3>(Bs, wn * TWN + y * 16, kk, lane);
+#pragma unroll
+      for (int x = 0; x < MX; ++x) {
+        const bf16x8_t af = read_frag3<AKC, BM3>(As, wm * TWM + x * 16, kk, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int y = 0; y < NY; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[y], af, acc[x][y], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    rd = rd + 1 == NSTAGE ? 0 : rd + 1;
+    wr = wr + 1 == NSTAGE ? 0 : wr + 1;
+    if (NSTAGE == 2) {                                     // 2-deep ring: the slot just read is refilled next
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < MX; ++x) {
+#pragma unroll
+    for (int y = 0; y < NY; ++y) {
+      const int64_t i = i0 + wm * TWM + x * 16 + (lane & 15);
+      const int64_t j = j0 + wn * TWN + y * 16 + 4 * (lane >> 4);
+      float v[4] = {acc[x][y][0], acc[x][y][1], acc[x][y][2], acc[x][y][3]};
+      if (g.ws) slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
+      else epilogue4<TO>(e, i, j, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // f32 MFMA kernel (exact fp32; generic strides; any M/N/K)
 // ------------------------------------------------------------------------------------------------------------
 constexpr int FBM = 64, FBK = 16, FPAD = 4;
@@ -362,7 +702,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// v3 needs > 64 KiB of dynamic LDS: raise the per-kernel limit once per instantiation.
+template <class K>
+void allow_lds(K kernel, size_t bytes) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    done = true;
+  }
+}
+
 bool aligned(const void* p, int a) { return p == nullptr || (((uintptr_t)p) % a) == 0; }
+
+// VIT_GEMM_IMPL=1 selects the register-staged v1 bf16 kernel (A/B comparisons); default 2 (LDS-DMA).
+// VIT_GEMM_IMPL selects the bf16 kernel for A/B runs: 1 = register-staged, 2 = LDS-DMA 128x128 (default),
+// 3 = LDS-DMA 256-row tiles (experimental).
+int gemm_impl() {
+  const char* v = getenv("VIT_GEMM_IMPL");
+  if (v && v[0] >= '1' && v[0] <= '3') return v[0] - '0';
+  return 2;
+}
 
 }  // namespace
 
@@ -424,10 +784,50 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     const int64_t nkt = (d->k + BK - 1) / BK;
     g.kt_per_split = (nkt + split - 1) / split;
     dim3 grid((unsigned)tiles, (unsigned)split), block(256);
-#define LAUNCH_BF(AK, BKK)                                                                              \
-  do {                                                                                                  \
-    if (out_bf && split == 1) gemm_bf16_kernel<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e);           \
-    else gemm_bf16_kernel<AK, BKK, float><<<grid, block, 0, s>>>(g, e);                                 \
+    // operand extents in bytes (for the buffer-descriptor range check of the v2 kernel)
+    const int64_t a_bytes = (akc ? (d->m - 1) * d->lda + d->k : (d->k - 1) * d->lda + d->m) * 2;
+    const int64_t b_bytes = (bkc ? (d->n - 1) * d->ldb + d->k : (d->k - 1) * d->ldb + d->n) * 2;
+    // v2/v3 (LDS-DMA) need whole 64-deep k-tiles (split boundaries are k-tile aligned) and operands < 2 GiB
+    const int impl = gemm_impl();
+    const bool dma_ok = d->k % BK == 0 && a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL;
+    const bool v2 = impl == 2 && dma_ok;
+    const bool v3 = impl == 3 && dma_ok && d->m >= 256;
+    // v3 tile width: 256 when the N tiles divide evenly and there are enough tiles, else 128
+    const int bn3 = getenv("VIT_GEMM_BN256") ? 256 : 128;
+    const int64_t tiles3 = ((d->m + 255) / 256) * ((d->n + bn3 - 1) / bn3);
+    int split3 = split;
+    GemmArgs g3 = g;
+    g3.tiles_n = (d->n + bn3 - 1) / bn3;
+    g3.kt_per_split = (nkt + split3 - 1) / split3;
+    dim3 grid3((unsigned)tiles3, (unsigned)split3);
+    const size_t lds3 = (size_t)(bn3 == 128 ? 3 : 2) * (256 + bn3) * BK * 2;
+#define LAUNCH_BF(AK, BKK)                                                                                     \
+  do {                                                                                                         \
+    if (v3) {                                                                                                  \
+      if (bn3 == 256) {                                                                                        \
+        if (out_bf && split == 1) {                                                                            \
+          allow_lds(gemm_bf16_v3<AK, BKK, 256, bf16_t>, lds3);                                                 \
+          gemm_bf16_v3<AK, BKK, 256, bf16_t><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                \
+        } else {                                                                                               \
+          allow_lds(gemm_bf16_v3<AK, BKK, 256, float>, lds3);                                                  \
+          gemm_bf16_v3<AK, BKK, 256, float><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                 \
+        }                                                                                                      \
+      } else {                                                                                                 \
+        if (out_bf && split == 1) {                                                                            \
+          allow_lds(gemm_bf16_v3<AK, BKK, 128, bf16_t>, lds3);                                                 \
+          gemm_bf16_v3<AK, BKK, 128, bf16_t><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                \
+        } else {                                                                                               \
+          allow_lds(gemm_bf16_v3<AK, BKK, 128, float>, lds3);                                                  \
+          gemm_bf16_v3<AK, BKK, 128, float><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                 \
+        }                                                                                                      \
+      }                                                                                                        \
+    } else if (v2) {                                                                                           \
+      if (out_bf && split == 1) gemm_bf16_v2<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);     \
+      else gemm_bf16_v2<AK, BKK, float><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);      \
+    } else {                                                                                                   \
+      if (out_bf && split == 1) gemm_bf16_kernel<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e);                \
+      else gemm_bf16_kernel<AK, BKK, float><<<grid, block, 0, s>>>(g, e);                                      \
+    }                                                                                                          \
   } while (0)
     if (akc && bkc) LAUNCH_BF(true, true);
     else if (akc && !bkc) LAUNCH_BF(true, false);

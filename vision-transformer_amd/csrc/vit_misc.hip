@@ -152,6 +152,13 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ 
   }
 }
 
+template <class T>
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                       T* __restrict__ dx, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    st1<T>(dx + t, ld1<T>(y + t) > 0.f ? ld1<T>(dy + t) : 0.f);
+}
+
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
     y[t] = gelu_erf(x[t]);
@@ -318,6 +325,15 @@ extern "C" int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n,
   if (dtype == VIT_BF16) dropout_bwd_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, thr, scale, seed);
   else dropout_bwd_kernel<float><<<grid, 256, 0, s>>>((const float*)x, (float*)y, n, thr, scale, seed);
   return vit::check_launch("vit_dropout_bwd");
+}
+
+extern "C" int vit_relu_bwd(const void* dy, const void* y, void* dx, int32_t dtype, int64_t n, void* stream) {
+  VIT_REQUIRE(dy && y && dx && n > 0, "vit_relu_bwd: bad arguments");
+  const unsigned grid = grid_for(n, 256, 16384);
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16) relu_bwd_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)y, (bf16_t*)dx, n);
+  else relu_bwd_kernel<float><<<grid, 256, 0, s>>>((const float*)dy, (const float*)y, (float*)dx, n);
+  return vit::check_launch("vit_relu_bwd");
 }
 
 extern "C" int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream) {
