@@ -136,3 +136,16 @@ def test_notebook_sdpa_kat(golden_dir):
     Q, K, V = emb @ w[..., 0:2], emb @ w[..., 2:4], emb @ w[..., 4:6]
     s = torch.softmax(Q @ K.transpose(-2, -1) / 2 ** 0.5, -1)
     np.testing.assert_allclose((s @ V).numpy(), np.array(k["expected_out"]), atol=6e-4)
+
+
+def test_seq_chain_variant_is_the_same_function(golden_dir):
+    """The summation-order variant used for tolerance scales computes the same model (micro goldens, fp32)."""
+    g = _npz(golden_dir, "micro.npz")
+    cfg = O.make_config("micro", img=32, batch=4)
+    st = O.init_state(cfg, 0)
+    logits, loss, grads = O.loss_and_grads(st, torch.from_numpy(g["x"]), torch.from_numpy(g["y"]), cfg,
+                                           seq_chain=True)
+    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=5e-5)
+    for k, v in grads.items():
+        ref = g["grad/" + k]
+        np.testing.assert_allclose(v.numpy(), ref, atol=1e-4 * max(1.0, float(np.abs(ref).max())), err_msg=k)

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box pass: gpu tests, smoke, bench (+cpu baseline), rocprofv3 kernel stats of a short bench.
+# Every GPU step has its own time limit; a crash/abort/timeout (exit >= 124 or signal) stops the script.
+# usage: bash tools/gpu_check.sh TAG [tests|bench|prof ...]
+set -u
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests smoke bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; }
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > "$OUT/tests.log" 2>&1 ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+            python bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof.log" 2>&1 ;;
+    *) echo "unknown step $s"; continue ;;
+  esac
+  rc=$?
+  echo "$s rc=$rc" | tee -a "$OUT/status.txt"
+  if fatal $rc; then echo "stopping after fatal rc=$rc in $s"; exit $rc; fi
+done
+exit 0
