@@ -163,7 +163,7 @@ def main():
             "step_mfma_frac": round(imgs * gf * 1e9 / (world * peak), 4),
             "gflop_per_image": round(gf, 3),
             "final_loss": round(final_loss, 4),
-            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel<true,true,bf16> (FFN fc1 forward)",
+            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_v4<true,true,bf16> (FFN fc1 forward)",
                          "achieved": round(fc1_flop / kavg / 1e12, 2) if kavg > 0 else None,
                          "peak": peak / 1e12, "unit": "TFLOP/s",
                          "frac": round(fc1_flop / kavg / peak, 4) if kavg > 0 else None,

@@ -69,6 +69,10 @@ typedef struct vit_gemm_desc {
 } vit_gemm_desc;
 
 int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d);
+/* Recommended split_k for C[m][n] with reduction depth k and input dtype (VIT_BF16 / VIT_F32) on the kernel vit_gemm
+ * will pick: fills one round of the 256 CUs with output tiles x K-slices, each slice >= 4 (bf16) / 8 (f32)
+ * k-tiles deep.  Used for the weight-gradient GEMMs (reduction over B*T rows; transformer.py Linear backward). */
+int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dtype);
 int vit_gemm(const vit_gemm_desc* d, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------

@@ -40,6 +40,41 @@ def test_gemm_bf16_exact_integers(akc, bkc, M, N, K):
     assert torch.equal(C.double(), ref), (C.double() - ref).abs().max()
 
 
+@pytest.mark.parametrize("impl", ["2", "4"])
+@pytest.mark.parametrize("akc,bkc", LAYOUTS)
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 264, 640), (1000, 776, 128), (72, 520, 192),
+                                   (2048, 768, 768)])
+def test_gemm_bf16_kernels_exact(monkeypatch, impl, akc, bkc, M, N, K):
+    """Every LDS-DMA kernel variant (VIT_GEMM_IMPL) on ragged M/N tails and 1..12 k-tiles, exact on integers."""
+    monkeypatch.setenv("VIT_GEMM_IMPL", impl)
+    g = torch.Generator().manual_seed(M + 5 * N + 11 * K)
+    A = _ints((M, K) if akc else (K, M), gen=g)
+    B = _ints((N, K) if bkc else (K, N), gen=g)
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    _ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), N, a_kcontig=akc, b_kcontig=bkc)
+    ref = _ref_op(A, B, akc, bkc)
+    assert torch.equal(C.double(), ref), (C.double() - ref).abs().max()
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)      # bf16 output path of the same kernel
+    _ops.gemm(A, B, Cb, M, N, K, A.stride(0), B.stride(0), N, a_kcontig=akc, b_kcontig=bkc)
+    assert torch.equal(Cb, ref.float().bfloat16())
+
+
+@pytest.mark.parametrize("impl", ["2", "4"])
+@pytest.mark.parametrize("split", [3, 7])
+def test_gemm_bf16_kernels_split_k(monkeypatch, impl, split):
+    """wgrad form with split-K (incl. an empty last slice: 10 k-tiles over 7 slices) on each kernel variant."""
+    monkeypatch.setenv("VIT_GEMM_IMPL", impl)
+    g = torch.Generator().manual_seed(split)
+    M, N, K = 264, 776, 640
+    A = _ints((K, M), gen=g)
+    B = _ints((K, N), gen=g)
+    C = _ints((M, N), gen=g, dtype=torch.float32)
+    ref = C.double() * 1.0 + _ref_op(A, B, False, False)
+    ws = torch.empty(split * M * N, dtype=torch.float32, device=DEV)
+    _ops.gemm(A, B, C, M, N, K, M, N, N, a_kcontig=False, b_kcontig=False, beta=1.0, split_k=split, workspace=ws)
+    assert torch.equal(C.double(), ref), (C.double() - ref).abs().max()
+
+
 def test_gemm_bf16_rejects_unaligned_contiguous_dim():
     A = torch.zeros(24, 50, dtype=torch.bfloat16, device=DEV)   # rowstrided A with M = 50 (not a multiple of 8)
     B = torch.zeros(24, 40, dtype=torch.bfloat16, device=DEV)

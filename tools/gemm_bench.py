@@ -24,11 +24,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--impls", default="2,3")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--no-ref", action="store_true", help="skip the hipBLASLt row")
     args = ap.parse_args()
     impls = args.impls.split(",")
     torch.manual_seed(0)
     ws = torch.empty(64 << 20, dtype=torch.float32, device="cuda")
+    only = [x.strip() for x in args.only.split(",") if x.strip()]
     for name, m, n, k, akc, bkc in SHAPES:
+        if only and name not in only:
+            continue
         a = (torch.rand((m, k) if akc else (k, m), device="cuda") * 2 - 1).bfloat16()
         b = (torch.rand((n, k) if bkc else (k, n), device="cuda") * 2 - 1).bfloat16()
         wgrad = not akc
@@ -36,7 +41,7 @@ def main():
         split = 1
         if wgrad:
             from VisionTransformer._engine import split_k_for
-            split = split_k_for(m, n, k)
+            split = split_k_for(m, n, k, torch.bfloat16)
         res = {}
         outs = {}
         for rep in range(args.reps + 2):
@@ -55,7 +60,7 @@ def main():
         A = a if akc else a.t()
         Bm = b.t() if bkc else b
         tb = []
-        for rep in range(args.reps + 2):
+        for rep in range(0 if args.no_ref else args.reps + 2):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             torch.matmul(A, Bm)
@@ -68,8 +73,9 @@ def main():
         for impl in impls:
             t = sorted(res[impl])[len(res[impl]) // 2]
             line += f" | v{impl}: {t*1e6:8.1f}us {flop/t/1e12:7.1f} TF"
-        tbl = sorted(tb)[len(tb) // 2]
-        line += f" | hipBLASLt: {tbl*1e6:8.1f}us {flop/tbl/1e12:7.1f} TF"
+        if tb:
+            tbl = sorted(tb)[len(tb) // 2]
+            line += f" | hipBLASLt: {tbl*1e6:8.1f}us {flop/tbl/1e12:7.1f} TF"
         if len(impls) > 1:
             d = (outs[impls[0]] - outs[impls[1]]).abs().max().item()
             line += f" | maxdiff {d:.3g}"

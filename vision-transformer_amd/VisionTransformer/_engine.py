@@ -24,7 +24,7 @@ import weakref
 import torch
 import torch.distributed as dist
 
-from . import _ops
+from . import _lib, _ops
 from ._ops import ACT_NONE, ACT_RELU
 
 DROPOUT_P = 0.2          # transformer.py:35,53 (config.dropout is stored but unused by the reference)
@@ -60,12 +60,10 @@ class _Region:
         return off
 
 
-def split_k_for(m, n, k, kt=64):
-    """K split for a weight-gradient GEMM (reduction over B*T rows): ~1024 workgroups of 128x128 tiles (two per CU,
-    two rounds), each split >= 8 k-tiles deep, at most 32 slabs."""
-    tiles = ((m + 127) // 128) * ((n + 127) // 128)
-    nkt = (k + kt - 1) // kt
-    return max(1, min((1024 + tiles - 1) // tiles, max(1, nkt // 8), 32))
+def split_k_for(m, n, k, dtype=torch.bfloat16):
+    """K split for a weight-gradient GEMM (reduction over B*T rows), chosen by the library for the kernel it will
+    run (vit_gemm_split_k_hint: one round of output tiles x K-slices over the 256 CUs)."""
+    return int(_lib.load().vit_gemm_split_k_hint(m, n, k, _ops.dtype_code(dtype)))
 
 
 class Tape:
@@ -247,7 +245,7 @@ class Engine:
 
     def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta):
         """out[m][n] (+)= sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K."""
-        split = split_k_for(m, n, k)
+        split = split_k_for(m, n, k, dy.dtype)
         need = split * m * n * 4 if split > 1 else 0
         ws = self._workspace(need) if split > 1 else None
         _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,

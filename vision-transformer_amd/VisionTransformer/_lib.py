@@ -49,6 +49,7 @@ _SIGS = {
     "vit_last_error": (ctypes.c_char_p, []),
     "vit_gemm_workspace_bytes": (_I64, [ctypes.POINTER(GemmDesc)]),
     "vit_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDesc), _P]),
+    "vit_gemm_split_k_hint": (ctypes.c_int, [_I64, _I64, _I64, _I32]),
     "vit_im2col": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _I64, _I64, _I64, _I64, _P]),
     "vit_embed_cls": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _I64, _I64, _P]),
     "vit_layernorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64, _F, _I32, _P]),
