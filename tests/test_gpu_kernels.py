@@ -223,6 +223,29 @@ def test_attention_fwd_bwd(dtype, hd, T, amp):
     assert err <= tol * 5 * max(1.0, g.abs().max().item()), err
 
 
+@pytest.mark.parametrize("T", [1, 31, 32, 33, 197, 256])
+def test_attention_bwd_fused_matches_split(monkeypatch, T):
+    """The one-workgroup-per-(image, head) backward (T <= 256) against the split dQ / dK-dV kernels and fp64."""
+    torch.manual_seed(T)
+    B, H, hd = 2, 3, 64
+    D = H * hd
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).bfloat16()
+    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
+    d_o = torch.randn(B * T, D, device=DEV).bfloat16()
+    fused = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0)
+    monkeypatch.setenv("VIT_ATTN_BWD_SPLIT", "1")
+    split = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0)
+    x = qkv.double().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    p = torch.softmax((q @ k.transpose(-1, -2)) * 8.0, -1)
+    (p @ v).permute(0, 2, 1, 3).reshape(B * T, D).backward(d_o.double())
+    g = x.grad
+    ef = (fused.double() - g).abs().max().item()
+    es = (split.double() - g).abs().max().item()
+    assert ef <= max(2 * es, 1e-2 * max(1.0, g.abs().max().item())), (ef, es)
+    assert (fused.float() - split.float()).abs().max().item() <= 2e-2 * max(1.0, g.abs().max().item())
+
+
 def test_attention_probs_generic():
     torch.manual_seed(5)
     B, T, H, hd = 2, 17, 2, 64

@@ -13,6 +13,8 @@
 //   reads and the transposed reads.
 // Other dtypes / head sizes — generic VALU kernels (exact fp32 arithmetic order per row), also used when the
 // `.attention_probs` tensor is requested.
+#include <stdlib.h>
+
 #include "vit_common.h"
 
 namespace {
@@ -534,6 +536,265 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Fused backward for T <= 256 (ViT: T = 197): one 8-wave workgroup per (image, head), everything from LDS.
+//   LDS: K, Q, dO as [Tp][64] images (Tp = T rounded up to 32, rows >= T zero), lse2 / delta per query, and a
+//   double-buffered dS^T image [Tp keys][32 queries].  delta = rowsum(dO * O) is computed here (no separate pass).
+//   Wave w owns key block w (32 keys: its K / V fragments live in registers, dK / dV accumulate in registers) and
+//   walks the query blocks qb:  S^T, dP^T (keys on lanes) -> P, dS -> dV += dO^T P, dK += Q^T dS, dS^T -> LDS;
+//   barrier; then dQ[qb] (32 x 64) is split over the 8 waves as 16x16 tiles (16x16x32 MFMA over all Tp keys):
+//   no recomputation of P, no atomics, no cross-wave reduction — deterministic.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int FB_TMAX = 256;
+
+VIT_DEV __amdgpu_buffer_rsrc_t make_rsrc_b(const void* base, int64_t bytes) {
+  const uint32_t nrec = bytes >= 0x7fffffffLL ? 0x7fffffffu : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, 0x00020000);
+}
+
+// A operand (16x16x32) of X^T from a [row][64] image: lane holds X[r0 + 8(lane>>4) + j][c0 + (lane&15)] for
+// j = 0..7, via two transposed reads (rows +0..3, +4..7).  `rowlen` = elements per image row; `swz` = chunk swizzle.
+template <int ROWLEN, bool ASWZ>
+VIT_DEV bf16x8_t col_frag16(const bf16_t* img, int r0, int c0, int lane) {
+  const int g = lane >> 4, lg = lane & 15, q = lg >> 2, p = lg & 3;
+  const int col = c0 + 4 * p;
+  const int c = col >> 3;
+  const int ra = r0 + 8 * g + q, rb = ra + 4;
+  const int ca = ASWZ ? (c ^ aswz(ra)) : c, cb = ASWZ ? (c ^ aswz(rb)) : c;
+  s16x4 lo = tr_read(img + ra * ROWLEN + (ca << 3) + (col & 7));
+  s16x4 hi = tr_read(img + rb * ROWLEN + (cb << 3) + (col & 7));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// LDS-DMA of one [Tp][64] head slice (rows of a row-major matrix with leading dim ld, columns col0..col0+63)
+// into a swizzled [Tp][64] image: 1 KiB pieces of 8 rows, lane-linear destination, the chunk swizzle applied to
+// the source address; rows >= Tn are zero-filled by an out-of-range offset.
+VIT_DEV void dma_head_slice(__amdgpu_buffer_rsrc_t rs, int64_t row0, int64_t ld, int64_t col0, int Tn, int Tp,
+                            bf16_t* img, int wave, int lane) {
+  for (int pc = wave; pc < Tp / 8; pc += 8) {
+    const int r = pc * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ aswz(r);
+    const uint32_t off = r < Tn ? (uint32_t)(2 * ((row0 + r) * ld + col0 + c * 8)) : 0x80000000u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + pc * 512), 16, off,
+                                             0, 0, 0);
+  }
+}
+
+// Row-contiguous store of a [rows][64] bf16 LDS image (plain [r][64], no swizzle) to global rows (row stride ld):
+// 8 lanes per 128-B row.
+VIT_DEV void store_rows64(const bf16_t* img, int rows, int valid_rows, bf16_t* dst, int64_t ld, int tid,
+                          int nthreads) {
+  for (int q = tid; q < rows * 8; q += nthreads) {
+    const int r = q >> 3, c = q & 7;
+    if (r < valid_rows)
+      *reinterpret_cast<uint4*>(dst + (int64_t)r * ld + c * 8) = *reinterpret_cast<const uint4*>(img + r * 64 + c * 8);
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+                                                         const bf16_t* __restrict__ d_o, const float* __restrict__ lse,
+                                                         bf16_t* __restrict__ dqkv, int64_t Tn64, int64_t H,
+                                                         float scale) {
+  constexpr int IMG = FB_TMAX * HD;                   // elements per [Tp][64] image (max)
+  constexpr int DST = FB_TMAX * 32;                   // elements per dS^T image [Tp][32]
+  constexpr int QST = 32 * HD;                        // dQ block staging [32][64]
+  __shared__ __attribute__((aligned(16))) bf16_t smem[3 * IMG + 2 * DST + 2 * QST + 2 * FB_TMAX * 2];
+  bf16_t* Ks = smem;
+  bf16_t* Qs = Ks + IMG;
+  bf16_t* Gs = Qs + IMG;
+  bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]; holds the O image during staging
+  bf16_t* dQs = dSt + 2 * DST;                         // [2][32][64]
+  float* lse2s = reinterpret_cast<float*>(dQs + 2 * QST);
+  float* dlts = lse2s + FB_TMAX;
+
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Tn = (int)Tn64;
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * HD, ld = 3 * D;
+  const int Tp = (Tn + 31) & ~31;
+  const int nqb = Tp / 32;
+  const float c2 = scale * LOG2E;
+
+  // ---- stage K, Q, dO, O (O into the dS region: only needed for delta); lse
+  {
+    const int64_t nb = gridDim.x / H;                  // host guarantees both tensors are < 2 GiB
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc_b(qkv, nb * Tn * ld * 2);
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc_b(d_o, nb * Tn * D * 2);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc_b(o, nb * Tn * D * 2);
+    dma_head_slice(rq, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane);
+    dma_head_slice(rq, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
+    dma_head_slice(rg, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
+    dma_head_slice(ro, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);
+  }
+  for (int r = tid; r < Tp; r += 512) lse2s[r] = r < Tn ? lse[bh * Tn + r] * LOG2E : INFINITY;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // delta[q] = sum_d dO[q][d] O[q][d]: 8 lanes per row (one 16-B chunk each), fixed shuffle-tree order
+  for (int q = tid; q < Tp * 8; q += 512) {
+    const int r = q >> 3, c = q & 7;
+    const int off = r * HD + ((c ^ aswz(r)) << 3);
+    const s16x8 vo = *reinterpret_cast<const s16x8*>(dSt + off);
+    const s16x8 vg = *reinterpret_cast<const s16x8*>(Gs + off);
+    float sacc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sacc += bf2f((bf16_t)vo[j]) * bf2f((bf16_t)vg[j]);
+    sacc += __shfl_xor(sacc, 1, 64);
+    sacc += __shfl_xor(sacc, 2, 64);
+    sacc += __shfl_xor(sacc, 4, 64);
+    if (c == 0) dlts[r] = sacc;
+  }
+  __syncthreads();                                    // delta visible; the O image (dS region) is dead
+
+  const bool kact = wave < nqb;                       // this wave owns key block `wave`
+  const int kb = wave * 32;
+  const int key = kb + (lane & 31);
+  const bool kmask = kb + 32 > Tn;                    // wave-uniform: this key block has keys >= T
+  const float kbias = key < Tn ? 0.f : -INFINITY;
+  const int dd = wave >> 1, qh = wave & 1;            // this wave's dQ tile: d 16dd.., queries 16qh..
+  bf16x8_t kf[4], vf[4];
+  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+  if (kact) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = row_frag(Ks, kb, s, lane);
+      vf[s] = glb_frag(qkv + b * Tn * ld, ld, kb, Tn, 2 * D + h * HD, s, lane);
+    }
+  }
+  // Per-lane LDS offsets (elements) inside a 32-row block: the row swizzle aswz(r) only uses bits 1..3 of r, so a
+  // block starting at a multiple of 16 rows adds rb * 64 and nothing else.
+  int rf_off[4];                                       // row_frag: row (lane&31), chunk 2s + hf
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int r = lane & 31;
+    rf_off[s] = r * HD + (((2 * s + hf) ^ aswz(r)) << 3);
+  }
+  int tf_off[2][2];                                    // tr_frag rows r1 / r1 + 8, d block db
+  {
+    const int G = lane >> 4, hh = G >> 1, lg = lane & 15, q = lg >> 2, pp = lg & 3;
+    const int r1 = 4 * hh + q, r2 = r1 + 8;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int col = db * 32 + 16 * (G & 1) + 4 * pp;
+      const int c = col >> 3;
+      tf_off[db][0] = r1 * HD + ((c ^ aswz(r1)) << 3) + (pp & 1) * 4;
+      tf_off[db][1] = r2 * HD + ((c ^ aswz(r2)) << 3) + (pp & 1) * 4;
+    }
+  }
+  int cf_k[2], cf_s[2];                                // col_frag16 on K (dQ A operand) and on dS^T (B operand)
+  {
+    const int g = lane >> 4, lg = lane & 15, q = lg >> 2, pp = lg & 3;
+    const int ra = 8 * g + q, rb2 = ra + 4;
+    const int colk = dd * 16 + 4 * pp, cols = qh * 16 + 4 * pp;
+    cf_k[0] = ra * HD + (((colk >> 3) ^ aswz(ra)) << 3) + (colk & 7);
+    cf_k[1] = rb2 * HD + (((colk >> 3) ^ aswz(rb2)) << 3) + (colk & 7);
+    cf_s[0] = ra * 32 + cols;
+    cf_s[1] = rb2 * 32 + cols;
+  }
+  auto trd = [&](const bf16_t* base, int o1, int o2) {
+    s16x4 lo = tr_read(base + o1);
+    s16x4 hi = tr_read(base + o2);
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  auto rrd = [&](const bf16_t* base, int o) {
+    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(base + o));
+  };
+
+  // pair(qb): this wave's key block against query block qb -> dV, dK accumulate; dS^T block -> dSt[qb & 1]
+  auto pair = [&](int qb) {
+    const int q0 = qb * 32;
+    const bf16_t* Qb = Qs + q0 * HD;
+    const bf16_t* Gb = Gs + q0 * HD;
+    f32x16 sacc = {}, pacc = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sacc = mfma32(rrd(Qb, rf_off[s]), kf[s], sacc);           // S[q][key]: lane = key
+      pacc = mfma32(rrd(Gb, rf_off[s]), vf[s], pacc);           // dP[q][key]
+    }
+    // registers 4g..4g+3 <-> queries q0 + 8g + 4hf + 0..3: broadcast b128 reads of the statistics
+    float p[16], ds[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2s + q0 + 8 * g + 4 * hf);
+      const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dlts + q0 + 8 * g + 4 * hf);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + i;
+        // queries >= T have lse2 = +inf -> P = 0 exactly
+        p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lv[i]);
+        ds[r] = pacc[r] - dv4[i];
+      }
+    }
+    if (kmask) {                                      // keys >= T (zero K rows) must not contribute
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lse2s[q0 + acc_row(r, hf)] + kbias);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ds[r] *= p[r];
+    const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      dv[db] = mfma32(trd(Gb, tf_off[db][0], tf_off[db][1]), p0, dv[db]);
+      dv[db] = mfma32(trd(Gb + 16 * HD, tf_off[db][0], tf_off[db][1]), p1, dv[db]);
+      dk[db] = mfma32(trd(Qb, tf_off[db][0], tf_off[db][1]), d0, dk[db]);
+      dk[db] = mfma32(trd(Qb + 16 * HD, tf_off[db][0], tf_off[db][1]), d1, dk[db]);
+    }
+    bf16_t* dS = dSt + (qb & 1) * DST + key * 32 + 4 * hf;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      float v4[4] = {ds[4 * g4], ds[4 * g4 + 1], ds[4 * g4 + 2], ds[4 * g4 + 3]};
+      st4<bf16_t>(dS + 8 * g4, v4);
+    }
+  };
+
+  // software pipeline: iteration i computes pair(i) (if any) and dQ(i-1) between the same two barriers
+  bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
+  for (int it = 0; it <= nqb; ++it) {
+    if (it >= 2) {                                    // dQ(it-2) staged in the previous iteration: full-row stores
+      const int qs = (it - 2) * 32;
+      store_rows64(dQs + ((it - 2) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
+    }
+    if (kact && it < nqb) pair(it);
+    if (it >= 1) {
+      const int qb = it - 1;
+      const bf16_t* dS = dSt + (qb & 1) * DST;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < Tp; kc += 32) {
+        const bf16x8_t a = trd(Ks + kc * HD, cf_k[0], cf_k[1]);
+        const bf16x8_t bq = trd(dS + kc * 32, cf_s[0], cf_s[1]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc, 0, 0, 0);
+      }
+      // D[m = d][n = q]: lane -> q = 16qh + (lane&15), d = 16dd + 4(lane>>4) + i  -> staging [32][64]
+      float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
+      st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * 64 + dd * 16 + 4 * (lane >> 4), v4);
+    }
+    __syncthreads();
+  }
+  {                                                   // last dQ block
+    const int qs = (nqb - 1) * 32;
+    store_rows64(dQs + ((nqb - 1) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
+  }
+  // dK, dV: [Tp][64] images in the (dead) Q and dO regions, then full-row stores
+  if (kact) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
+                      dk[db][4 * g + 3] * scale};
+        float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+        st4<bf16_t>(Qs + key * 64 + db * 32 + 8 * g + 4 * hf, a);
+        st4<bf16_t>(Gs + key * 64 + db * 32 + 8 * g + 4 * hf, c);
+      }
+    }
+  }
+  __syncthreads();
+  store_rows64(Qs, Tp, Tn, dqkv + b * Tn * ld + D + h * HD, ld, tid, 512);
+  store_rows64(Gs, Tp, Tn, dqkv + b * Tn * ld + 2 * D + h * HD, ld, tid, 512);
+}
+
 bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }
 
 }  // namespace
@@ -568,7 +829,10 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, con
   VIT_REQUIRE(qkv && o && d_o && lse && dqkv && workspace && B > 0 && T > 0 && H > 0 && hd > 0,
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
-  if (use_mfma(dtype, hd)) {
+  if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_BWD_SPLIT")) {
+    attn_bwd_fused<<<(unsigned)(B * H), 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse,
+                                                     (bf16_t*)dqkv, T, H, scale);
+  } else if (use_mfma(dtype, hd)) {
     float* delta = (float*)workspace;
     const int64_t rows = B * T * H;
     attn_delta<<<(unsigned)std::min<int64_t>((rows + 255) / 256, 8192), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)d_o,
