@@ -66,6 +66,14 @@ def split_k_for(m, n, k, dtype=torch.bfloat16):
     return int(_lib.load().vit_gemm_split_k_hint(m, n, k, _ops.dtype_code(dtype)))
 
 
+def head_split_for(m, n, k):
+    """K split for the classifier head's fp32 GEMMs (M = batch rows only): ~1024 workgroups of the 64x64 fp32
+    tile, each slice >= 8 k-steps of 16.  Without it these few-tile GEMMs run one long dependent k-loop per CU."""
+    tiles = ((m + 63) // 64) * ((n + 63) // 64)
+    nkt = (k + 15) // 16
+    return max(1, min((1024 + tiles - 1) // tiles, nkt // 8, 32))
+
+
 class Tape:
     """Activations saved by a training forward."""
     __slots__ = ("B", "cols", "blocks", "z", "u", "gz", "zn", "mh", "rh", "seed", "training")
@@ -251,6 +259,18 @@ class Engine:
         _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
                   split_k=split, workspace=ws)
 
+    def _head_gemm(self, a, b, c, m, n, k, lda, ldb, ldc, **kw):
+        split = head_split_for(m, n, k)
+        ws = self._workspace(split * m * n * 4) if split > 1 else None
+        _ops.gemm(a, b, c, m, n, k, lda, ldb, ldc, split_k=split, workspace=ws, **kw)
+
+    def _head_linear(self, x, w, bias):
+        m, k = x.shape
+        n = w.shape[0]
+        y = torch.empty(m, n, dtype=x.dtype, device=x.device)
+        self._head_gemm(x, w, y, m, n, k, x.stride(0), w.stride(0), n, bias=bias)
+        return y
+
     def _colsum(self, x, rows, cols, ld, out, beta):
         _ops.colsum(x, rows, cols, ld, out, beta=beta)
 
@@ -336,10 +356,10 @@ class Engine:
         # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
         z = torch.empty(B, D, dtype=torch.float32, device=x.device)
         _ops.copy2d(xcur, T * D, z, D, B, D)
-        u = _ops.linear(z, prm["h0_w"], bias=prm["h0_b"])
+        u = self._head_linear(z, prm["h0_w"], prm["h0_b"])
         gz = _ops.gelu_fwd(u)
         zn, mh, rh = _ops.layernorm_fwd(gz, prm["hln_w"], prm["hln_b"], eps=LN_EPS)
-        logits = _ops.linear(zn, prm["h3_w"], bias=prm["h3_b"])
+        logits = self._head_linear(zn, prm["h3_w"], prm["h3_b"])
         if save:
             tape.B, tape.cols, tape.blocks = B, cols, blocks
             tape.z, tape.u, tape.gz, tape.zn, tape.mh, tape.rh = z, u, gz, zn, mh, rh
@@ -380,7 +400,7 @@ class Engine:
         nc = self.nc
         # ---- head (fp32)
         dzn = torch.empty(B, 4 * D, dtype=torch.float32, device=dev)
-        _ops.gemm(dlogits, prm["h3_w"], dzn, B, 4 * D, nc, nc, 4 * D, 4 * D, b_kcontig=False)
+        self._head_gemm(dlogits, prm["h3_w"], dzn, B, 4 * D, nc, nc, 4 * D, 4 * D, b_kcontig=False)
         self._wgrad(dlogits, tape.zn, gw["h3_w"], nc, 4 * D, B, nc, 4 * D, beta)
         self._colsum(dlogits, B, nc, nc, gw["h3_b"], beta)
         dgz = torch.empty_like(tape.gz)
@@ -389,7 +409,7 @@ class Engine:
         self._colsum(part[1], part.shape[1], 4 * D, 4 * D, gw["hln_b"], beta)
         du = _ops.gelu_bwd(tape.u, dgz)
         dz = torch.empty(B, D, dtype=torch.float32, device=dev)
-        _ops.gemm(du, prm["h0_w"], dz, B, D, 4 * D, 4 * D, D, D, b_kcontig=False)
+        self._head_gemm(du, prm["h0_w"], dz, B, D, 4 * D, 4 * D, D, D, b_kcontig=False)
         self._wgrad(du, tape.z, gw["h0_w"], 4 * D, D, B, 4 * D, D, beta)
         self._colsum(du, B, 4 * D, 4 * D, gw["h0_b"], beta)
         self._bucket_ready(self.head_range)

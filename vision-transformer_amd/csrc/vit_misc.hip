@@ -106,11 +106,29 @@ __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ x, in
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_stage2(const float* __restrict__ part, int64_t nchunks, int64_t cols,
-                                                     float* __restrict__ out, float beta) {
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < cols; c += (int64_t)gridDim.x * blockDim.x) {
+// Stage 2: 64 columns per block; 16 waves stride over the chunk partials (wave w sums chunks w, w+16, ...), then the
+// 16 wave sums are added in wave order through LDS -> deterministic for a given (rows, cols).
+constexpr int CS2_WAVES = 16;
+__global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2(const float* __restrict__ part, int64_t nchunks,
+                                                                int64_t cols, float* __restrict__ out, float beta) {
+  __shared__ float red[CS2_WAVES][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < cols) {
+    int64_t k = w;
+    for (; k + CS2_WAVES < nchunks; k += 2 * CS2_WAVES) {   // two independent chains per lane
+      s0 += part[k * cols + c];
+      s1 += part[(k + CS2_WAVES) * cols + c];
+    }
+    if (k < nchunks) s0 += part[k * cols + c];
+  }
+  red[w][lane] = s0 + s1;
+  __syncthreads();
+  if (w == 0 && c < cols) {
     float s = 0.f;
-    for (int64_t k = 0; k < nchunks; ++k) s += part[k * cols + c];
+#pragma unroll
+    for (int i = 0; i < CS2_WAVES; ++i) s += red[i][lane];
     out[c] = beta != 0.f ? beta * out[c] + s : s;
   }
 }
@@ -293,7 +311,7 @@ extern "C" int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t row
     colsum_stage1<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
   else
     colsum_stage1<float><<<g1, 256, 0, s>>>((const float*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
-  colsum_stage2<<<grid_for(cols, 256), 256, 0, s>>>((const float*)workspace, ch, cols, out, beta);
+  colsum_stage2<<<(unsigned)((cols + 63) / 64), 64 * CS2_WAVES, 0, s>>>((const float*)workspace, ch, cols, out, beta);
   return vit::check_launch("vit_colsum");
 }
 

@@ -6,7 +6,7 @@
 
 namespace {
 
-constexpr int LN_BWD_PARTS_MAX = 512;
+constexpr int LN_BWD_PARTS_MAX = 2048;
 
 template <class T, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int64_t ldx,
@@ -178,7 +178,7 @@ int ln_fwd_launch(const T* x, int64_t ldx, const float* g, const float* b, T* y,
 
 extern "C" int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols) {
   (void)cols;
-  int64_t p = (rows + 15) / 16;  // >= 16 rows (4 per wave) per block
+  int64_t p = (rows + 15) / 16;  // >= 16 rows (4 per wave) per block; up to 2048 blocks (8 waves/SIMD in flight)
   if (p > LN_BWD_PARTS_MAX) p = LN_BWD_PARTS_MAX;
   if (p < 1) p = 1;
   return p;
