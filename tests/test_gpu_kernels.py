@@ -75,6 +75,29 @@ def test_gemm_bf16_kernels_split_k(monkeypatch, impl, split):
     assert torch.equal(C.double(), ref), (C.double() - ref).abs().max()
 
 
+@pytest.mark.parametrize("variant", ["plain", "bias_relu", "bias_gelu", "aux", "bias_drop_res", "drop_res_f32",
+                                     "alpha"])
+def test_gemm_epilogue_kinds_match_general(monkeypatch, variant):
+    """The specialised v4 epilogues are bitwise equal to the general one (VIT_GEMM_EPI_GENERAL=1)."""
+    torch.manual_seed(7)
+    M, N, K = 1000, 776, 256
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    res32 = torch.randn(M, N, device=DEV)
+    kw = {"plain": {}, "bias_relu": dict(bias=bias, act=_ops.ACT_RELU), "bias_gelu": dict(bias=bias, act=_ops.ACT_GELU),
+          "aux": dict(aux=aux, ldaux=N), "bias_drop_res": dict(bias=bias, dropout_p=0.2, seed=99, res=aux, ldres=N),
+          "drop_res_f32": dict(dropout_p=0.3, seed=5, res=res32, ldres=N), "alpha": dict(alpha=0.37)}[variant]
+    outs = []
+    for general in ("0", "1"):
+        monkeypatch.setenv("VIT_GEMM_EPI_GENERAL", general)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        _ops.gemm(x, w, out, M, N, K, K, K, N, **kw)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_bf16_rejects_unaligned_contiguous_dim():
     A = torch.zeros(24, 50, dtype=torch.bfloat16, device=DEV)   # rowstrided A with M = 50 (not a multiple of 8)
     B = torch.zeros(24, 40, dtype=torch.bfloat16, device=DEV)

@@ -452,174 +452,6 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_v2(GemmArgs g, EpiParams e, 
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// bf16 MFMA kernel v3: 256 x BN x 64 workgroup tile (BN = 256 or 128), 8 waves (512 threads), LDS-DMA staging
-// with hoisted per-lane offsets, 2 LDS stages (BN=256: 128 KiB -> one workgroup per CU, two waves per SIMD).
-//   Bytes staged per FLOP: 1/2 (BN=256) or 2/3 (BN=128) of the 128x128 tile's — the operand stream per CU, not the
-//   MFMA rate, is what limits the smaller tile.
-//   Wave grid: BN=256 -> 2 (M) x 4 (N) waves of 128x64; BN=128 -> 4 x 2 waves of 64x64.
-//   LDS images: k-contiguous operand [R rows][64 k] (128-B rows, chunk ^ (row & 7)); row-strided operand
-//   [64 k][R] (2R-B rows, chunk ^ swz_rs(k) on the low 4 chunk bits) — the same conflict analysis as v1 since every
-//   row starts on bank 0.
-// ------------------------------------------------------------------------------------------------------------
-template <bool KC, int R>
-VIT_DEV void dma_offsets3(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int wave, int lane, uint32_t* off) {
-  constexpr int NP = R / 64;                 // pieces per wave: (R*64*2 B) / 1 KiB / 8 waves
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int ii = wave * NP + i;
-    int64_t gr, gk;
-    if (KC) {
-      const int r = ii * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      gr = r0 + r;
-      gk = k0 + c * 8;
-    } else {
-      constexpr int RPP = 1024 / (2 * R);    // k-rows per piece
-      constexpr int CPR = R / 8;             // 16-B chunks per k-row
-      const int kr = ii * RPP + lane / CPR;
-      const int c = (lane % CPR) ^ swz_rs(kr);
-      gk = k0 + kr;
-      gr = r0 + c * 8;
-    }
-    const int64_t eoff = KC ? gr * ld + gk : gk * ld + gr;
-    off[i] = gr < rows ? (uint32_t)(eoff * 2) : OOB;
-  }
-}
-
-template <int NP>
-VIT_DEV void dma_issue3(__amdgpu_buffer_rsrc_t rs, const uint32_t* off, uint32_t soff, bf16_t* lds_tile, int wave) {
-#pragma unroll
-  for (int i = 0; i < NP; ++i)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        rs, (__attribute__((address_space(3))) void*)(lds_tile + (wave * NP + i) * 512), 16, off[i], soff, 0, 0);
-}
-
-// fragment of 16 rows starting at rb0 (k-step kk) from an R-row image
-template <bool KC, int R>
-VIT_DEV bf16x8_t read_frag3(const bf16_t* lds, int rb0, int kk, int lane) {
-  if (KC) {
-    const int r = rb0 + (lane & 15);
-    const int c = kk * 4 + (lane >> 4);
-    s16x8 v = *reinterpret_cast<const s16x8*>(lds + r * BK + ((c ^ (r & 7)) << 3));
-    return __builtin_bit_cast(bf16x8_t, v);
-  } else {
-    const int lg = lane & 15, q = lg >> 2, p = lg & 3, g = lane >> 4;
-    const int kr = kk * 32 + 8 * g + q;
-    const int c = (rb0 + 4 * p) >> 3;
-    const int sw = swz_rs(kr);
-    s16x4 lo = tr_read(lds + kr * R + ((c ^ sw) << 3) + (p & 1) * 4);
-    s16x4 hi = tr_read(lds + (kr + 4) * R + ((c ^ sw) << 3) + (p & 1) * 4);
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  }
-}
-
-template <int N>
-VIT_DEV void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <bool AKC, bool BKC, int BN3, class TO>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_v3(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
-  constexpr int BM3 = 256;
-  constexpr int NSTAGE = BN3 == 128 ? 3 : 2;              // LDS ring depth (3 x 48 KiB / 2 x 64 KiB)
-  constexpr int WN = BN3 == 256 ? 4 : 2, WM = 8 / WN;     // wave grid
-  constexpr int TWM = BM3 / WM, TWN = BN3 / WN;           // wave tile
-  constexpr int MX = TWM / 16, NY = TWN / 16;              // 16x16 fragments per wave
-  constexpr int NPA = BM3 / 64, NPB = BN3 / 64;            // LDS-DMA pieces per wave per k-tile
-  constexpr int NPT = NPA + NPB;
-  constexpr int A_ELEMS = BM3 * BK, B_ELEMS = BN3 * BK, STAGE = A_ELEMS + B_ELEMS;
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem3[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int64_t nwg = gridDim.x, orig = blockIdx.x;
-  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int64_t tm = bid / g.tiles_n, tn = bid % g.tiles_n;
-  const int64_t i0 = tm * BM3, j0 = tn * BN3;
-  const int64_t nkt = g.K / BK;
-  const int64_t kt0 = (int64_t)blockIdx.y * g.kt_per_split;
-  const int nk = (int)(min(nkt, kt0 + g.kt_per_split) - kt0);
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
-  const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
-  const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
-  uint32_t oa[NPA], ob[NPB];
-  dma_offsets3<AKC, BM3>(g.lda, g.M, i0, kt0 * BK, wave, lane, oa);
-  dma_offsets3<BKC, BN3>(g.ldb, g.N, j0, kt0 * BK, wave, lane, ob);
-
-  f32x4 acc[MX][NY];
-#pragma unroll
-  for (int x = 0; x < MX; ++x)
-#pragma unroll
-    for (int y = 0; y < NY; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: k-tiles 0 .. NSTAGE-2 in flight
-  uint32_t soa = 0, sob = 0;
-#pragma unroll
-  for (int st = 0; st < NSTAGE - 1; ++st) {
-    if (st < nk) {
-      dma_issue3<NPA>(ra, oa, soa, smem3 + st * STAGE, wave);
-      dma_issue3<NPB>(rb, ob, sob, smem3 + st * STAGE + A_ELEMS, wave);
-    }
-    soa += sa;
-    sob += sb;
-  }
-  int rd = 0, wr = NSTAGE - 1;                             // ring slots: read (k-tile kt), write (k-tile kt+NSTAGE-1)
-  for (int kt = 0; kt < nk; ++kt) {
-    // k-tile kt landed for this wave: leave the younger NSTAGE-2 tiles' pieces in flight (counted, never 0 in the
-    // steady state), then a raw barrier (no vmcnt(0) drain) makes every wave's pieces visible.
-    if (NSTAGE == 3 && kt + 1 < nk) wait_vmcnt<NPT>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // refill the slot read in iteration kt-1 (every wave is past that iteration's reads: the barrier above)
-    if (kt + NSTAGE - 1 < nk) {
-      dma_issue3<NPA>(ra, oa, soa, smem3 + wr * STAGE, wave);
-      dma_issue3<NPB>(rb, ob, sob, smem3 + wr * STAGE + A_ELEMS, wave);
-    }
-    soa += sa;
-    sob += sb;
-    const bf16_t* As = smem3 + rd * STAGE;
-    const bf16_t* Bs = As + A_ELEMS;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8_t bfr[NY];
-#pragma unroll
-      for (int y = 0; y < NY; ++y) bfr[y] = read_frag3<BKC, BN3>(Bs, wn * TWN + y * 16, kk, lane);
-#pragma unroll
-      for (int x = 0; x < MX; ++x) {
-        const bf16x8_t af = read_frag3<AKC, BM3>(As, wm * TWM + x * 16, kk, lane);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int y = 0; y < NY; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[y], af, acc[x][y], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    rd = rd + 1 == NSTAGE ? 0 : rd + 1;
-    wr = wr + 1 == NSTAGE ? 0 : wr + 1;
-    if (NSTAGE == 2) {                                     // 2-deep ring: the slot just read is refilled next
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-#pragma unroll
-  for (int x = 0; x < MX; ++x) {
-#pragma unroll
-    for (int y = 0; y < NY; ++y) {
-      const int64_t i = i0 + wm * TWM + x * 16 + (lane & 15);
-      const int64_t j = j0 + wn * TWN + y * 16 + 4 * (lane >> 4);
-      float v[4] = {acc[x][y][0], acc[x][y][1], acc[x][y][2], acc[x][y][3]};
-      if (g.ws) slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
-      else epilogue4<TO>(e, i, j, v);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------
 // bf16 MFMA kernel v4: 256x256x64 tile, 8 waves in two ping-pong groups, one LDS-DMA half-tile per phase.
 //
 //   LDS (one 128 KiB array): 2 k-tile buffers x 4 half-tiles {A rows 0-127, A rows 128-255, B rows 0-127,
@@ -641,6 +473,69 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v3(GemmArgs g, EpiParams e, 
 //   read was >= 2 phases earlier.
 // ------------------------------------------------------------------------------------------------------------
 constexpr int HALF = 128 * BK;            // elements per half-tile image (16 KiB)
+
+// Epilogue specialisations of v4 (chosen on the host; every one computes exactly what epilogue4 computes for the
+// arguments it is chosen for).  Rows are written full-width from the LDS image, with per-column state (bias) loaded
+// once per tile instead of once per row.
+enum EpiKind : int {
+  EPI_PLAIN = 0,      // alpha * acc
+  EPI_BIAS_ACT = 1,   // act(alpha * acc + bias)
+  EPI_AUX = 2,        // alpha * acc masked by aux > 0 (ReLU backward)
+  EPI_BDR = 3,        // dropout(alpha * acc [+ bias]) [+ res]
+  EPI_SLAB = 4,       // split-K fp32 slab
+  EPI_GENERAL = 5     // epilogue4 (beta, row groups, row-modulo residual, unaligned, any combination)
+};
+
+template <class TO, int KIND>
+VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_t j, const float (&b4)[4], bool relu,
+                        bool gelu, float v[4]) {
+  if (KIND == EPI_GENERAL) {
+    epilogue4<TO>(e, i, j, v);
+    return;
+  }
+  if (KIND == EPI_SLAB) {
+    slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
+    return;
+  }
+  if (i >= e.m || j >= e.n) return;                 // fast kinds: n % 4 == 0 and 16-B aligned rows (e.vec)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] *= e.alpha;
+  if (KIND == EPI_BIAS_ACT || KIND == EPI_BDR) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += b4[r];
+  }
+  if (KIND == EPI_BIAS_ACT) {
+    if (relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    } else if (gelu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+    }
+  }
+  if (KIND == EPI_AUX) {
+    float a[4];
+    if (e.aux_dtype == VIT_BF16) ld4<bf16_t>((const bf16_t*)e.aux + i * e.ldaux + j, a);
+    else ld4<float>((const float*)e.aux + i * e.ldaux + j, a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
+  }
+  if (KIND == EPI_BDR) {
+    if (e.use_drop) {
+      const uint32_t base = (uint32_t)(i * e.n + j);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = vit_hash_u32(e.seed, base + r) >= e.drop_thr ? v[r] * e.drop_scale : 0.f;
+    }
+    if (e.res) {
+      float a[4];
+      if (e.res_dtype == VIT_BF16) ld4<bf16_t>((const bf16_t*)e.res + i * e.ldres + j, a);
+      else ld4<float>((const float*)e.res + i * e.ldres + j, a);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += a[r];
+    }
+  }
+  st4<TO>((TO*)e.c + i * e.ldc + j, v);
+}
 
 template <bool KC>
 VIT_DEV void dma_offsets4(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int wave, int lane, uint32_t (&off)[2]) {
@@ -708,7 +603,7 @@ VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <bool AKC, bool BKC, class TO>
+template <bool AKC, bool BKC, class TO, int KIND>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
   __shared__ __attribute__((aligned(16))) bf16_t smem4[2 * 4 * HALF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -817,8 +712,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 #ifdef VIT_GEMM_NOEPI
           if (v[0] != 1234.5f) continue;
 #endif
-          if (g.ws) slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
-          else epilogue4<TO>(e, i, j, v);
+          v4_epi_row<TO, EPI_GENERAL>(e, g, i, j, v, false, false, v);
         }
 #else
   // Row-contiguous epilogue through LDS, one 128-row half of the tile per pass: the fragment layout (16 rows x 32 B
@@ -826,6 +720,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   // loads are full-line.  Image: [128][256] fp32, 16-B chunk index XOR (row & 15) -> conflict-free b128 writes
   // (8 rows per lane group) and reads (16 chunks of one row per group).
   float* ep = reinterpret_cast<float*>(smem4);
+  const int64_t jcol = j0 + 4 * lane;
+  float b4[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias && jcol < e.n) ld4<float>(e.bias + jcol, b4);
+  const bool relu = e.act == VIT_ACT_RELU, gelu = e.act == VIT_ACT_GELU;
   __syncthreads();                                        // every wave's k-loop LDS reads are done, no DMA pending
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
@@ -849,8 +747,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 #ifdef VIT_GEMM_NOEPI
       if (v[0] != 1234.5f) continue;
 #endif
-      if (g.ws) slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
-      else epilogue4<TO>(e, i, j, v);
+      v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v);
     }
     if (mh == 0) __syncthreads();
   }
@@ -940,21 +837,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// v3 needs > 64 KiB of dynamic LDS: raise the per-kernel limit once per instantiation.
-template <class K>
-void allow_lds(K kernel, size_t bytes) {
-  static bool done = false;
-  if (!done) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bytes);
-    done = true;
-  }
-}
-
 bool aligned(const void* p, int a) { return p == nullptr || (((uintptr_t)p) % a) == 0; }
 
-// bf16 kernels: 1 = register-staged 128x128, 2 = LDS-DMA 128x128, 3 = LDS-DMA 256-row (experimental),
-// 4 = LDS-DMA 256x256 ping-pong with LDS-staged epilogue.
+// bf16 kernels: 1 = register-staged 128x128, 2 = LDS-DMA 128x128, 4 = LDS-DMA 256x256 ping-pong with LDS-staged
+// epilogue (3 = 4: the former 256-row experiment was removed).
 // VIT_GEMM_IMPL forces a kernel (A/B runs and the per-variant tests); 0 / unset = automatic: v4 when both output
 // dims span a 256 tile, else v2.
 int gemm_impl_env() {
@@ -1047,51 +933,39 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     // operand extents in bytes (for the buffer-descriptor range check of the v2 kernel)
     const int64_t a_bytes = (akc ? (d->m - 1) * d->lda + d->k : (d->k - 1) * d->lda + d->m) * 2;
     const int64_t b_bytes = (bkc ? (d->n - 1) * d->ldb + d->k : (d->k - 1) * d->ldb + d->n) * 2;
-    // v2/v3 (LDS-DMA) need whole 64-deep k-tiles (split boundaries are k-tile aligned) and operands < 2 GiB
+    // v2/v4 (LDS-DMA) need whole 64-deep k-tiles (split boundaries are k-tile aligned) and operands < 2 GiB
     const int impl = gemm_impl(d->m, d->n);
     const bool dma_ok = d->k % BK == 0 && a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL;
     const bool v2 = impl == 2 && dma_ok;
-    const bool v3 = impl == 3 && dma_ok && d->m >= 256;
-    const bool v4 = impl == 4 && dma_ok;
+    const bool v4 = (impl == 4 || impl == 3) && dma_ok;
     GemmArgs g4 = g;
     g4.tiles_n = (d->n + 255) / 256;
     g4.kt_per_split = (nkt + split - 1) / split;
     dim3 grid4((unsigned)(((d->m + 255) / 256) * g4.tiles_n), (unsigned)split);
-    // v3 tile width: 256 when the N tiles divide evenly and there are enough tiles, else 128
-    const int bn3 = getenv("VIT_GEMM_BN256") ? 256 : 128;
-    const int64_t tiles3 = ((d->m + 255) / 256) * ((d->n + bn3 - 1) / bn3);
-    int split3 = split;
-    GemmArgs g3 = g;
-    g3.tiles_n = (d->n + bn3 - 1) / bn3;
-    g3.kt_per_split = (nkt + split3 - 1) / split3;
-    dim3 grid3((unsigned)tiles3, (unsigned)split3);
-    const size_t lds3 = (size_t)(bn3 == 128 ? 3 : 2) * (256 + bn3) * BK * 2;
+    // v4 epilogue kind
+    const bool fast = e.vec && e.grp == 0 && e.res_rowmod == 0 && e.beta == 0.f;
+    int kind = EPI_GENERAL;
+    if (split > 1) kind = EPI_SLAB;
+    else if (fast && !e.bias && e.act == VIT_ACT_NONE && !e.aux && !e.use_drop && !e.res) kind = EPI_PLAIN;
+    else if (fast && e.bias && !e.aux && !e.use_drop && !e.res) kind = EPI_BIAS_ACT;
+    else if (fast && e.aux && !e.bias && e.act == VIT_ACT_NONE && !e.use_drop && !e.res) kind = EPI_AUX;
+    else if (fast && !e.aux && e.act == VIT_ACT_NONE && (e.use_drop || e.res)) kind = EPI_BDR;
+    const char* dk = getenv("VIT_GEMM_EPI_GENERAL");      // A/B switch: force the general epilogue
+    if (dk && dk[0] == '1' && kind != EPI_SLAB) kind = EPI_GENERAL;
+#define V4(AK, BKK, TO, KIND) gemm_bf16_v4<AK, BKK, TO, KIND><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes)
 #define LAUNCH_BF(AK, BKK)                                                                                     \
   do {                                                                                                         \
     if (v4) {                                                                                                  \
-      if (out_bf && split == 1) gemm_bf16_v4<AK, BKK, bf16_t><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes);  \
-      else gemm_bf16_v4<AK, BKK, float><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes);                        \
-    } else if (v3) {                                                                                           \
-      if (bn3 == 256) {                                                                                        \
-        if (out_bf && split == 1) {                                                                            \
-          allow_lds(gemm_bf16_v3<AK, BKK, 256, bf16_t>, lds3);                                                 \
-          gemm_bf16_v3<AK, BKK, 256, bf16_t><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                \
-        } else {                                                                                               \
-          allow_lds(gemm_bf16_v3<AK, BKK, 256, float>, lds3);                                                  \
-          gemm_bf16_v3<AK, BKK, 256, float><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                 \
-        }                                                                                                      \
-      } else {                                                                                                 \
-        if (out_bf && split == 1) {                                                                            \
-          allow_lds(gemm_bf16_v3<AK, BKK, 128, bf16_t>, lds3);                                                 \
-          gemm_bf16_v3<AK, BKK, 128, bf16_t><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                \
-        } else {                                                                                               \
-          allow_lds(gemm_bf16_v3<AK, BKK, 128, float>, lds3);                                                  \
-          gemm_bf16_v3<AK, BKK, 128, float><<<grid3, 512, lds3, s>>>(g3, e, a_bytes, b_bytes);                 \
-        }                                                                                                      \
-      }                                                                                                        \
+      if (kind == EPI_SLAB) V4(AK, BKK, float, EPI_SLAB);                                                      \
+      else if (!out_bf) V4(AK, BKK, float, EPI_GENERAL);                                                       \
+      else if (kind == EPI_PLAIN) V4(AK, BKK, bf16_t, EPI_PLAIN);                                              \
+      else if (AK && BKK && kind == EPI_BIAS_ACT) V4(AK, BKK, bf16_t, EPI_BIAS_ACT);                           \
+      else if (AK && BKK && kind == EPI_BDR) V4(AK, BKK, bf16_t, EPI_BDR);                                     \
+      else if (AK && !BKK && kind == EPI_AUX) V4(AK, BKK, bf16_t, EPI_AUX);                                    \
+      else V4(AK, BKK, bf16_t, EPI_GENERAL);                                                                   \
     } else if (v2) {                                                                                           \
       if (out_bf && split == 1) gemm_bf16_v2<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);     \
-      else gemm_bf16_v2<AK, BKK, float><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);      \
+      else gemm_bf16_v2<AK, BKK, float><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);                         \
     } else {                                                                                                   \
       if (out_bf && split == 1) gemm_bf16_kernel<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e);                \
       else gemm_bf16_kernel<AK, BKK, float><<<grid, block, 0, s>>>(g, e);                                      \
@@ -1101,6 +975,7 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     else if (akc && !bkc) LAUNCH_BF(true, false);
     else LAUNCH_BF(false, false);
 #undef LAUNCH_BF
+#undef V4
   } else {
     g.tiles_n = (d->n + FBM - 1) / FBM;
     const int64_t tiles = ((d->m + FBM - 1) / FBM) * g.tiles_n;
