@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--no-ref", action="store_true", help="skip the hipBLASLt row")
+    ap.add_argument("--epi", action="store_true", help="apply the engine's fused epilogue of each shape "
+                    "(bias+ReLU, bias+dropout+residual, ReLU-backward mask)")
     args = ap.parse_args()
     impls = args.impls.split(",")
     torch.manual_seed(0)
@@ -42,6 +44,16 @@ def main():
         if wgrad:
             from VisionTransformer._engine import split_k_for
             split = split_k_for(m, n, k, torch.bfloat16)
+        kw = {}
+        if args.epi and not wgrad:
+            bias = torch.randn(n, device="cuda")
+            if name == "fwd fc1":
+                kw = dict(bias=bias, act=_ops.ACT_RELU)
+            elif name in ("fwd proj", "fwd fc2"):
+                kw = dict(bias=bias, res=torch.randn(m, n, device="cuda").bfloat16(), ldres=n, dropout_p=0.2,
+                          seed=7)
+            elif name == "dgrad fc2":
+                kw = dict(aux=torch.randn(m, n, device="cuda").bfloat16(), ldaux=n)
         res = {}
         outs = {}
         for rep in range(args.reps + 2):
@@ -50,7 +62,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 _ops.gemm(a, b, c, m, n, k, a.stride(0), b.stride(0), n, a_kcontig=akc, b_kcontig=bkc,
-                          split_k=split, workspace=ws)
+                          split_k=split, workspace=ws, **kw)
                 e1.record()
                 torch.cuda.synchronize()
                 if rep >= 2:

@@ -486,9 +486,35 @@ enum EpiKind : int {
   EPI_GENERAL = 5     // epilogue4 (beta, row groups, row-modulo residual, unaligned, any combination)
 };
 
+// Kinds whose row epilogue reads a second [m][n]-shaped bf16 operand (ReLU mask / residual).  Those reads are
+// issued for all 32 rows a wave owns BEFORE the accumulators go through LDS (raw bf16x4 per lane and row), so the
+// epilogue pays one memory latency per tile instead of one per group of rows — each dependent load also waited for
+// every store issued before it (one vmcnt counter).
+template <int KIND>
+VIT_DEV bool v4_has_pre(const EpiParams& e) {
+  return KIND == EPI_AUX || (KIND == EPI_BDR && e.res != nullptr);
+}
+
+template <int KIND>
+VIT_DEV uint2 v4_pre_load(const EpiParams& e, int64_t i, int64_t j) {
+  uint2 r = make_uint2(0u, 0u);
+  if (i < e.m && j < e.n) {
+    const bf16_t* p = KIND == EPI_AUX ? (const bf16_t*)e.aux + i * e.ldaux + j : (const bf16_t*)e.res + i * e.ldres + j;
+    r = *reinterpret_cast<const uint2*>(p);
+  }
+  return r;
+}
+
+VIT_DEV void unpack_bf16x4(uint2 u, float (&a)[4]) {
+  a[0] = __uint_as_float(u.x << 16);
+  a[1] = __uint_as_float(u.x & 0xffff0000u);
+  a[2] = __uint_as_float(u.y << 16);
+  a[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+
 template <class TO, int KIND>
 VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_t j, const float (&b4)[4], bool relu,
-                        bool gelu, float v[4]) {
+                        bool gelu, float v[4], uint2 pre = make_uint2(0u, 0u)) {
   if (KIND == EPI_GENERAL) {
     epilogue4<TO>(e, i, j, v);
     return;
@@ -513,10 +539,9 @@ VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_
       for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
     }
   }
-  if (KIND == EPI_AUX) {
+  if (KIND == EPI_AUX) {                            // aux is bf16 (host-checked), prefetched
     float a[4];
-    if (e.aux_dtype == VIT_BF16) ld4<bf16_t>((const bf16_t*)e.aux + i * e.ldaux + j, a);
-    else ld4<float>((const float*)e.aux + i * e.ldaux + j, a);
+    unpack_bf16x4(pre, a);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
   }
@@ -526,10 +551,9 @@ VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = vit_hash_u32(e.seed, base + r) >= e.drop_thr ? v[r] * e.drop_scale : 0.f;
     }
-    if (e.res) {
+    if (e.res) {                                     // res is bf16 (host-checked), prefetched
       float a[4];
-      if (e.res_dtype == VIT_BF16) ld4<bf16_t>((const bf16_t*)e.res + i * e.ldres + j, a);
-      else ld4<float>((const float*)e.res + i * e.ldres + j, a);
+      unpack_bf16x4(pre, a);
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += a[r];
     }
@@ -724,6 +748,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   float b4[4] = {0.f, 0.f, 0.f, 0.f};
   if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias && jcol < e.n) ld4<float>(e.bias + jcol, b4);
   const bool relu = e.act == VIT_ACT_RELU, gelu = e.act == VIT_ACT_GELU;
+  // second-operand rows of both passes, in flight before the LDS round trip (see v4_has_pre)
+  uint2 pre[2][16];
+  const bool has_pre = v4_has_pre<KIND>(e);
+  if (has_pre) {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
+  }
   __syncthreads();                                        // every wave's k-loop LDS reads are done, no DMA pending
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
@@ -738,7 +771,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
           *reinterpret_cast<f32x4*>(ep + row * 256 + ((chunk ^ (row & 15)) << 2)) = acc[mh][nh][x][y];
         }
     __syncthreads();
-#pragma unroll 4
+#pragma unroll
     for (int rr = 0; rr < 16; ++rr) {
       const int row = wave * 16 + rr;
       const f32x4 a = *reinterpret_cast<const f32x4*>(ep + row * 256 + ((lane ^ (row & 15)) << 2));
@@ -747,7 +780,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 #ifdef VIT_GEMM_NOEPI
       if (v[0] != 1234.5f) continue;
 #endif
-      v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v);
+      v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
     }
     if (mh == 0) __syncthreads();
   }
@@ -948,8 +981,10 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     if (split > 1) kind = EPI_SLAB;
     else if (fast && !e.bias && e.act == VIT_ACT_NONE && !e.aux && !e.use_drop && !e.res) kind = EPI_PLAIN;
     else if (fast && e.bias && !e.aux && !e.use_drop && !e.res) kind = EPI_BIAS_ACT;
-    else if (fast && e.aux && !e.bias && e.act == VIT_ACT_NONE && !e.use_drop && !e.res) kind = EPI_AUX;
-    else if (fast && !e.aux && e.act == VIT_ACT_NONE && (e.use_drop || e.res)) kind = EPI_BDR;
+    else if (fast && e.aux && e.aux_dtype == VIT_BF16 && !e.bias && e.act == VIT_ACT_NONE && !e.use_drop && !e.res)
+      kind = EPI_AUX;
+    else if (fast && !e.aux && e.act == VIT_ACT_NONE && (e.use_drop || e.res) && (!e.res || e.res_dtype == VIT_BF16))
+      kind = EPI_BDR;
     const char* dk = getenv("VIT_GEMM_EPI_GENERAL");      // A/B switch: force the general epilogue
     if (dk && dk[0] == '1' && kind != EPI_SLAB) kind = EPI_GENERAL;
 #define V4(AK, BKK, TO, KIND) gemm_bf16_v4<AK, BKK, TO, KIND><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes)
