@@ -9,7 +9,8 @@ FusedAdamW step.  Weak scaling: every rank processes its own batch of 256.
         bench.py --gpus N --steps K --warmup W
 
 Rank 0 prints ONE JSON line.  `roofline` is measured live: HIP events on the compute stream bracket every launch of
-the dominant kernel family's representative GEMM (the FFN fc1 forward, M=B*T, N=4D, K=D) inside the timed steps.
+the dominant kernel family's representative GEMM (the fused QKV projection forward, M=B*T, N=3D, K=D: one launch of
+gemm_bf16_v4<kcontig, kcontig, bf16, EPI_PLAIN>) inside the timed steps.
 `cpu_baseline` times the oracle port (oracle/vit_oracle.py: the reference's algorithm restated in torch on CPU) on
 the host cores, rank 0 at N=1 only, on a bounded sample (ViT-B/16 224^2 fp32, batch 8, 1 warmup + 3 steps).
 """
@@ -97,11 +98,11 @@ def main():
     eng = model.hip_engine
     D, L, T, N = cfg.embedding_size, cfg.num_blocks, cfg.num_patches + 1, cfg.num_patches
     M = args.batch * T
-    fc1_flop = 2.0 * M * 4 * D * D
+    qkv_flop = 2.0 * M * 3 * D * D
     events = []
 
     def hook(name, phase):
-        if name == "fc1_fwd":
+        if name == "qkv_fwd":
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             events.append(ev)
@@ -163,11 +164,11 @@ def main():
             "step_mfma_frac": round(imgs * gf * 1e9 / (world * peak), 4),
             "gflop_per_image": round(gf, 3),
             "final_loss": round(final_loss, 4),
-            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_v4<true,true,bf16> (FFN fc1 forward)",
-                         "achieved": round(fc1_flop / kavg / 1e12, 2) if kavg > 0 else None,
+            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_v4<true,true,bf16,0> (fused QKV projection forward)",
+                         "achieved": round(qkv_flop / kavg / 1e12, 2) if kavg > 0 else None,
                          "peak": peak / 1e12, "unit": "TFLOP/s",
-                         "frac": round(fc1_flop / kavg / peak, 4) if kavg > 0 else None,
-                         "flop_per_launch": fc1_flop, "avg_launch_us": round(kavg * 1e6, 2),
+                         "frac": round(qkv_flop / kavg / peak, 4) if kavg > 0 else None,
+                         "flop_per_launch": qkv_flop, "avg_launch_us": round(kavg * 1e6, 2),
                          "launches_timed": len(kdur), "traffic": None},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 1
+#define VIT_ABI_VERSION 3
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1 } vit_dtype;
@@ -66,8 +66,15 @@ typedef struct vit_gemm_desc {
   int64_t out_group_rows, out_group_stride;
   void* workspace;
   int64_t workspace_bytes;
+  /* NULL, or [ceil(m/256)][n] f32: per-256-row-block column sums of C as stored (after the epilogue and the
+   * out_dtype rounding) — the bias gradient of the layer whose input gradient C is (transformer.py Linear backward),
+   * finished by vit_colsum_finish.  Requires out_group_rows == 0. */
+  float* colsum_part;
 } vit_gemm_desc;
 
+/* Workspace vit_gemm can use: split_k > 1: the K-split fp32 slabs (required).  split_k <= 1: the slabs of the split-K
+ * tail (when the 256x256 tiles leave the last round of the 256 CUs at most half full, those tile rows run split-K
+ * over the idle CUs; VIT_GEMM_TAIL=0 disables it), or 0.  Without it (NULL / too small) the GEMM runs unsplit. */
 int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d);
 /* Recommended split_k for C[m][n] with reduction depth k and input dtype (VIT_BF16 / VIT_F32) on the kernel vit_gemm
  * will pick: fills one round of the 256 CUs with output tiles x K-slices, each slice >= 4 (bf16) / 8 (f32)
@@ -93,15 +100,17 @@ int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, i
  *   bwd: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
  *        dx_out = dx (+ dres when dres != NULL)                    — fused residual-gradient add (transformer.py:77-78)
  *        drop_out = dx_out * keep(drop_seed, i*cols + j) / (1-p)    — fused dropout backward of the producer branch
- *        dgamma/dbeta: per-workgroup partials in `partial` [2][nparts][cols], reduced by vit_colsum (deterministic).
+ *        dgamma/dbeta: per-workgroup partials in `partial` [2][nparts][cols], reduced by vit_colsum_finish
+ *        (deterministic); with `osum` != 0 also partial [2] = column sums of the stored gradient output (drop_out
+ *        when given, else dx_out) — the bias gradient of the Linear that consumes it, so [3][nparts][cols].
  * ------------------------------------------------------------------------------------------------------------ */
 int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma, const float* beta, void* y, int64_t ldy,
                       float* mean, float* rstd, int64_t rows, int64_t cols, float eps, int32_t dtype, void* stream);
 int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols);
 int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
                       const float* mean, const float* rstd, const void* dres, void* dx_out, void* drop_out,
-                      float drop_p, uint32_t drop_seed, float* partial, int64_t rows, int64_t cols, int32_t dtype,
-                      void* stream);
+                      float drop_p, uint32_t drop_seed, float* partial, int32_t osum, int64_t rows, int64_t cols,
+                      int32_t dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------
  * Multi-head self-attention (transformer.py:9-31 per head, :44-45 concat): qkv[B*T][3*D] with Q at columns
@@ -121,6 +130,8 @@ int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, const float* l
 /* ------------------------------------------------------------------------------------------------------------
  * Reductions / elementwise.
  *   vit_colsum: out[j] = beta*out[j] + sum_i x[i*ldx + j]  (bias / pos / LN-affine gradients); deterministic.
+ *   vit_colsum_finish: outs[s][j] = beta*outs[s][j] + sum_p part[s][p][j] for s < nsets (<= 3), summed in a fixed
+ *               order — second stage of the column sums fused into vit_gemm (colsum_part) / vit_layernorm_bwd.
  *   vit_copy2d: dst[orow(i)*ldd + j] = beta*dst + src[irow(i)*lds + j] with optional row grouping on the source
  *               (irow(i) = (i/G)*Gs + i%G) — token-0 gather (vit.py:80), CLS-gradient copy, dropout-free casts.
  *   vit_dropout_bwd: y = x * keep(seed, i) / (1-p)  (transformer.py:47,59 backward).
@@ -131,6 +142,8 @@ int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, const float* l
 int64_t vit_colsum_workspace_bytes(int64_t rows, int64_t cols);
 int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t cols, float* out, float beta,
                void* workspace, void* stream);
+int vit_colsum_finish(const float* part, int64_t nparts, int64_t cols, int32_t nsets, float* out0, float* out1,
+                      float* out2, float beta, void* stream);
 int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,
                int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
                void* stream);

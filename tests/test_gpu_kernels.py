@@ -197,11 +197,24 @@ def test_layernorm_fwd_bwd(dtype, cols):
     yr.backward(dy.float())
     dx = torch.empty_like(x)
     drop = torch.empty_like(x)
-    part = _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, drop_out=drop, drop_p=0.2, drop_seed=99)
+    part = _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, drop_out=drop, drop_p=0.2, drop_seed=99,
+                              osum=True)
     dg = torch.empty(cols, device=DEV)
     db = torch.empty(cols, device=DEV)
     _ops.colsum(part[0], part.shape[1], cols, cols, dg)
-    _ops.colsum(part[1], part.shape[1], cols, cols, db)
+    ds = torch.full((cols,), 0.5, device=DEV)
+    _ops.colsum_finish(part[1:], [db, ds])
+    # third partial set: column sums of drop_out as stored (the bias gradient of the Linear it feeds)
+    ref_ds = drop.double().sum(0)
+    assert ((ds.double() - ref_ds).abs() <= 1e-5 * drop.double().abs().sum(0) + 1e-6).all()
+    # without drop_out the third set sums dx_out
+    dx2 = torch.empty_like(x)
+    part2 = _ops.layernorm_bwd(dy, x, g, mean, rstd, dx2, dres=dres, osum=True)
+    assert torch.equal(dx2, dx)
+    s3 = [torch.zeros(cols, device=DEV) for _ in range(3)]
+    _ops.colsum_finish(part2, s3)
+    assert ((s3[2].double() - dx.double().sum(0)).abs() <= 1e-5 * dx.double().abs().sum(0) + 1e-6).all()
+    assert torch.equal(s3[0], dg)
     ref_dx = xr.grad + dres.float()
     scale = ref_dx.abs().max().item()
     assert (dx.float() - ref_dx).abs().max().item() <= tol * 4 * scale
@@ -210,6 +223,66 @@ def test_layernorm_fwd_bwd(dtype, cols):
     from oracle.vit_oracle import dropout_keep
     keep = dropout_keep(99, (rows, cols)).to(DEV)
     assert torch.equal(drop.float(), (dx.float() * keep * 1.25).to(dtype).float())
+
+
+@pytest.mark.parametrize("variant", ["plain", "aux", "bias_relu", "bias_drop_res", "f32_out", "v2_small"])
+def test_gemm_colsum_part(variant):
+    """Column sums of C as stored, fused into the v4 row epilogue (a separate pass for the other kernels / general
+    epilogue), finished by vit_colsum_finish: the bias gradient of the Linear whose input gradient C is."""
+    torch.manual_seed(11)
+    M, N, K = (300, 200, 128) if variant == "v2_small" else (1000, 776, 256)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    out = torch.empty(M, N, dtype=torch.float32 if variant == "f32_out" else torch.bfloat16, device=DEV)
+    part = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
+    if variant == "aux":                                  # dgrad layout: B row-strided [K][N], ReLU-backward mask
+        wt = w.t().contiguous()
+        _ops.gemm(x, wt, out, M, N, K, K, N, N, b_kcontig=False, aux=aux, ldaux=N, colsum_part=part)
+    else:
+        kw = {"bias_relu": dict(bias=bias, act=_ops.ACT_RELU),
+              "bias_drop_res": dict(bias=bias, dropout_p=0.2, seed=3, res=aux, ldres=N)}.get(variant, {})
+        _ops.gemm(x, w, out, M, N, K, K, K, N, colsum_part=part, **kw)
+    got = torch.full((N,), 0.5, device=DEV)
+    _ops.colsum_finish(part, [got], beta=1.0)
+    ref = out.double().sum(0) + 0.5
+    assert ((got.double() - ref).abs() <= 1e-5 * out.double().abs().sum(0) + 1e-5).all()
+
+
+@pytest.mark.parametrize("variant", ["plain", "bias_relu", "aux", "bias_drop_res"])
+def test_gemm_split_k_tail(monkeypatch, variant):
+    """A v4 GEMM whose 256x256 tiles leave the last round of the 256 CUs at most half full runs the remaining tile
+    rows split-K (M = 23140, N = 768: 91 x 3 tiles = 85 tile rows in whole rounds + 6 tile rows split 3 ways).
+    Integer data: outputs and fused column sums equal the unsplit kernel's bit for bit, dropout masks included."""
+    import ctypes
+    from VisionTransformer import _lib
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 90 * 256 + 100, 768, 768
+    d = _lib.GemmDesc()
+    d.m, d.n, d.k, d.a_kcontig, d.b_kcontig, d.in_dtype, d.out_dtype = M, N, K, 1, 1, 1, 1
+    assert _lib.load().vit_gemm_workspace_bytes(ctypes.byref(d)) == 3 * (M - 85 * 256) * N * 4
+    a = _ints((M, K), gen=g)
+    b = _ints((N, K), gen=g)
+    bias = _ints((N,), gen=g, dtype=torch.float32)
+    aux = _ints((M, N), gen=g)
+    outs, parts = [], []
+    for tail in ("0", "1"):
+        monkeypatch.setenv("VIT_GEMM_TAIL", tail)
+        c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        p = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
+        if variant == "aux":
+            _ops.gemm(a, b.t().contiguous(), c, M, N, K, K, N, N, b_kcontig=False, aux=aux, ldaux=N, colsum_part=p)
+        else:
+            kw = {"bias_relu": dict(bias=bias, act=_ops.ACT_RELU),
+                  "bias_drop_res": dict(bias=bias, dropout_p=0.2, seed=9, res=aux, ldres=N)}.get(variant, {})
+            _ops.gemm(a, b, c, M, N, K, K, K, N, colsum_part=p, **kw)
+        outs.append(c)
+        parts.append(p)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(parts[0], parts[1])
+    if variant == "plain":
+        assert torch.equal(outs[1], (a.double() @ b.double().t()).float().bfloat16())
 
 
 def _attn_ref(qkv, B, T, H, hd, scale):
@@ -267,6 +340,23 @@ def test_attention_bwd_fused_matches_split(monkeypatch, T):
     es = (split.double() - g).abs().max().item()
     assert ef <= max(2 * es, 1e-2 * max(1.0, g.abs().max().item())), (ef, es)
     assert (fused.float() - split.float()).abs().max().item() <= 2e-2 * max(1.0, g.abs().max().item())
+
+
+@pytest.mark.parametrize("T", [1, 31, 32, 33, 197, 256])
+def test_attention_fwd_fused_matches_split(monkeypatch, T):
+    """The one-workgroup-per-(image, head) forward (T <= 256) against the 128-query-tile kernel and fp32."""
+    torch.manual_seed(T + 1)
+    B, H, hd = 2, 3, 64
+    qkv = (torch.randn(B * T, 3 * H * hd, device=DEV) * 0.5).bfloat16()
+    of, lf = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
+    monkeypatch.setenv("VIT_ATTN_FWD_SPLIT", "1")
+    osp, lsp = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
+    o_ref, lse_ref, _ = _attn_ref(qkv, B, T, H, hd, 8.0)
+    ef = (of.float() - o_ref).abs().max().item()
+    es = (osp.float() - o_ref).abs().max().item()
+    assert ef <= max(2 * es, 1e-2 * max(1.0, o_ref.abs().max().item())), (ef, es)
+    assert (lf - lse_ref).abs().max().item() <= 1e-3 * max(1.0, lse_ref.abs().max().item())
+    assert (lf - lsp).abs().max().item() <= 1e-3 * max(1.0, lsp.abs().max().item())
 
 
 def test_attention_probs_generic():

@@ -260,3 +260,23 @@ def test_vit_base_224_bf16_full_size_properties():
         opt.step()
         losses.append(loss.item())
     assert losses[2] < losses[0], losses
+
+
+def test_side_stream_weight_gradients_bitwise_equal():
+    """Weight gradients on the side stream (default) equal the in-order schedule bit for bit (train mode, bf16)."""
+    ocfg = O.make_config("micro", img=64, batch=4, blocks=2)
+    ocfg.embedding_size, ocfg.num_heads = 128, 2
+    st = O.init_state(ocfg, seed=4)
+    x, y = O.synthetic_batch(ocfg)
+    gs = []
+    for conc in (True, False):
+        m = _model(ocfg, dtype=torch.bfloat16)
+        m.load_state_dict(st)
+        m.train()
+        m.hip_engine.concurrent_wgrad = conc
+        torch.manual_seed(7)
+        loss = cross_entropy(m(x.to(DEV)), y.to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        gs.append(m.hip_engine.G.clone())
+    assert torch.equal(gs[0], gs[1])

@@ -19,6 +19,7 @@ Layouts (device):
 from __future__ import annotations
 
 import math
+import os
 import weakref
 
 import torch
@@ -103,6 +104,10 @@ class Engine:
         self._ver_sig = None
         self.stats = {"packs": 0}
         self.profile_hook = None          # callable(name, phase) around named launches (bench.py HIP events)
+        # weight-gradient GEMMs on a side stream (VIT_CONCURRENT_WGRAD=0: in order on the current stream)
+        self.concurrent_wgrad = os.environ.get("VIT_CONCURRENT_WGRAD", "1") != "0"
+        self._wstream = None
+        self._wws = None
 
     # ------------------------------------------------------------------------------------------------------------
     # layout
@@ -251,13 +256,38 @@ class Engine:
             self._ws = torch.empty(max(nbytes // 4 + 1, 1 << 20), dtype=torch.float32, device=self.device)
         return self._ws
 
-    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta):
-        """out[m][n] (+)= sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K."""
+    def _side_stream(self):
+        """HIP stream for the weight-gradient GEMMs of the backward (None: run them in order on the current stream).
+        A weight gradient depends only on tensors the current stream has already produced and nothing reads it
+        before the bucket all-reduce / the optimizer step, so on its own stream it runs beside the dgrad / attention
+        / LayerNorm chain and fills the CUs that chain leaves idle (partial last rounds of tiles, memory-bound
+        kernels).  Same kernels, same inputs: the gradients are bitwise those of the in-order schedule."""
+        if not self.concurrent_wgrad or self.device is None or self.device.type != "cuda":
+            return None
+        if self._wstream is None or self._wstream.device != self.device:
+            self._wstream = torch.cuda.Stream(device=self.device)
+        return self._wstream
+
+    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta, side=None):
+        """out[m][n] (+)= sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K.  With `side` it
+        runs on that stream after everything already enqueued on the current one."""
         split = split_k_for(m, n, k, dy.dtype)
         need = split * m * n * 4 if split > 1 else 0
-        ws = self._workspace(need) if split > 1 else None
+        if side is None:
+            ws = self._workspace(need) if split > 1 else None
+            _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
+                      split_k=split, workspace=ws)
+            return
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        ws = None
+        if need:
+            if self._wws is None or self._wws.numel() * 4 < need:
+                self._wws = torch.empty(max(need // 4 + 1, 1 << 20), dtype=torch.float32, device=self.device)
+            ws = self._wws
         _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
-                  split_k=split, workspace=ws)
+                  split_k=split, workspace=ws, stream=side)
+        for t in (dy, x) if ws is None else (dy, x, ws):
+            t.record_stream(side)          # the caching allocator must not hand these out before `side` is done
 
     def _head_gemm(self, a, b, c, m, n, k, lda, ldb, ldc, **kw):
         split = head_split_for(m, n, k)
@@ -331,7 +361,12 @@ class Engine:
             blk = model.transformer_encoder.blocks[l]
             x_in = xcur
             a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
+            hook = self.profile_hook
+            if hook:
+                hook("qkv_fwd", 0)
             qkv = _ops.linear(a1, self.ww[f"{l}.qkv_w"])                                # 3H heads' K/Q/V in one GEMM
+            if hook:
+                hook("qkv_fwd", 1)
             probs = None
             if want_probs:
                 probs = torch.empty(B, H, T, T, dtype=torch.float32, device=x.device)
@@ -341,12 +376,7 @@ class Engine:
             _ops.gemm(o, self.ww[f"{l}.proj_w"], x_mid, M, D, D, D, D, D, bias=prm[f"{l}.proj_b"], res=x_in,
                       ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 0))
             a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
-            hook = self.profile_hook
-            if hook:
-                hook("fc1_fwd", 0)
             h = _ops.linear(a2, self.ww[f"{l}.fc1_w"], bias=prm[f"{l}.fc1_b"], act=ACT_RELU)
-            if hook:
-                hook("fc1_fwd", 1)
             x_out = torch.empty(M, D, dtype=dt, device=x.device)
             _ops.gemm(h, self.ww[f"{l}.fc2_w"], x_out, M, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
                       res=x_mid, ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 1))
@@ -369,14 +399,22 @@ class Engine:
     # ------------------------------------------------------------------------------------------------------------
     # backward
     # ------------------------------------------------------------------------------------------------------------
-    def _bucket_ready(self, rng):
-        """Launch the all-reduce of one contiguous gradient range (RCCL stream waits on the compute stream)."""
+    def _bucket_ready(self, rng, side=None):
+        """Launch the all-reduce of one contiguous gradient range (RCCL stream waits on the compute stream, and on
+        the weight-gradient stream `side` when there is one)."""
         if self.ddp_enabled:
             a, b = rng
             if dist.get_backend(self.ddp_group) == "nccl":      # RCCL: native average
-                w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
+                if side is not None:                          # issued from `side`: the main chain does not wait
+                    side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(side):
+                        w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
+                else:
+                    w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
                 self._works.append((w, None))
             else:                                             # gloo (CPU tests): sum, scaled after the wait
+                if side is not None:
+                    torch.cuda.current_stream(self.device).wait_stream(side)
                 w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.SUM, group=self.ddp_group, async_op=True)
                 self._works.append((w, (a, b)))
 
@@ -421,43 +459,52 @@ class Engine:
             _ops.dropout_bwd(dx, g1, DROPOUT_P, site_seed(tape.seed, L - 1, 1))
         else:
             g1 = dx
+        side = self._side_stream()
+        g1_summed = False          # block L-1's fc2 bias gradient: g1 comes from the head (plain column sum below)
         for l in reversed(range(L)):
             x_in, a1, m1, r1, qkv, o, lse, x_mid, a2, m2, r2, h = tape.blocks[l]
             # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
+            self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side)
+            if not g1_summed:
+                self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta)
             dh = torch.empty(M, 4 * D, dtype=dt, device=dev)
+            dh_part = torch.empty(_ops.colsum_part_rows(M), 4 * D, dtype=torch.float32, device=dev)
+            # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
             _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=h,
-                      ldaux=4 * D)                                                        # relu backward fused
-            self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta)
-            self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta)
+                      ldaux=4 * D, colsum_part=dh_part)
+            _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
+            self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, M, 4 * D, D, beta, side)
             da2 = torch.empty(M, D, dtype=dt, device=dev)
             _ops.gemm(dh, self.ww[f"{l}.fc1_w"], da2, M, D, 4 * D, 4 * D, D, D, b_kcontig=False)
-            self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, M, 4 * D, D, beta)
-            self._colsum(dh, M, 4 * D, 4 * D, gw[f"{l}.fc1_b"], beta)
             dx_mid = torch.empty(M, D, dtype=dt, device=dev)
             g0 = torch.empty(M, D, dtype=dt, device=dev) if tape.training else None
+            # ln2 backward + residual add + dropout backward of the MHA branch; its third partial set is the column
+            # sums of g0 as stored = the proj bias gradient
             part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx,
-                                      drop_out=g0, drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l, 0))
-            self._colsum(part[0], part.shape[1], D, D, gw[f"{l}.ln2_w"], beta)
-            self._colsum(part[1], part.shape[1], D, D, gw[f"{l}.ln2_b"], beta)
+                                      drop_out=g0, drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l, 0), osum=True)
+            _ops.colsum_finish(part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta=beta)
             if g0 is None:
                 g0 = dx_mid
             # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
+            self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta, side)
             do = torch.empty(M, D, dtype=dt, device=dev)
             _ops.gemm(g0, self.ww[f"{l}.proj_w"], do, M, D, D, D, D, D, b_kcontig=False)
-            self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta)
-            self._colsum(g0, M, D, D, gw[f"{l}.proj_b"], beta)
             dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
                                  workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)))
+            self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side)
             da1 = torch.empty(M, D, dtype=dt, device=dev)
             _ops.gemm(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
-            self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta)
             dx_in = torch.empty(M, D, dtype=dt, device=dev)
             g1n = torch.empty(M, D, dtype=dt, device=dev) if (tape.training and l > 0) else None
+            # ln1 backward; for l > 0 its third partial set is the column sums of the next g1 (g1n, or dx_in in eval)
+            # = the fc2 bias gradient of block l-1
             part = _ops.layernorm_bwd(da1, x_in, prm[f"{l}.ln1_w"], m1, r1, dx_in, dres=dx_mid, drop_out=g1n,
-                                      drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l - 1, 1) if l > 0 else 0)
-            self._colsum(part[0], part.shape[1], D, D, gw[f"{l}.ln1_w"], beta)
-            self._colsum(part[1], part.shape[1], D, D, gw[f"{l}.ln1_b"], beta)
-            self._bucket_ready(self.block_range[l])
+                                      drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l - 1, 1) if l > 0 else 0,
+                                      osum=l > 0)
+            outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if l > 0 else [])
+            _ops.colsum_finish(part, outs, beta=beta)
+            g1_summed = l > 0
+            self._bucket_ready(self.block_range[l], side)
             dx = dx_in
             g1 = g1n if g1n is not None else dx_in
         # ---- embedding (vit.py:39-42): dx = d(x0) [B*T, D]
@@ -466,8 +513,10 @@ class Engine:
         dpatch = torch.empty(B * N, D, dtype=dt, device=dev)
         _ops.copy2d(dx, D, dpatch, D, B * N, D, group=(N, T))
         self._colsum(dpatch, B * N, D, D, gw["conv_b"], beta)
-        self._wgrad(dpatch, tape.cols, gw["conv_w"], D, self.CPP, B * N, D, self.CPP, beta)
-        self._bucket_ready(self.embed_range)
+        self._wgrad(dpatch, tape.cols, gw["conv_w"], D, self.CPP, B * N, D, self.CPP, beta, side)
+        self._bucket_ready(self.embed_range, side)
+        if side is not None:
+            torch.cuda.current_stream(dev).wait_stream(side)      # every weight gradient is in G before the step
         if self._works:
             self._finish_buckets()
 

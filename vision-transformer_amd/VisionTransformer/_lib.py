@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 3
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
@@ -33,6 +33,7 @@ class GemmDesc(ctypes.Structure):
         ("split_k", ctypes.c_int32),
         ("out_group_rows", ctypes.c_int64), ("out_group_stride", ctypes.c_int64),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
+        ("colsum_part", ctypes.c_void_p),
     ]
 
 
@@ -54,13 +55,14 @@ _SIGS = {
     "vit_embed_cls": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _I64, _I64, _P]),
     "vit_layernorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64, _F, _I32, _P]),
     "vit_layernorm_bwd_parts": (_I64, [_I64, _I64]),
-    "vit_layernorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _F, _U32, _P, _I64, _I64,
-                                         _I32, _P]),
+    "vit_layernorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _F, _U32, _P, _I32, _I64,
+                                         _I64, _I32, _P]),
     "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
     "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _P]),
     "vit_colsum_workspace_bytes": (_I64, [_I64, _I64]),
     "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _P, _P]),
+    "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),
     "vit_copy2d": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _I32, _I64, _I64, _I64, _I64, _F, _P]),
     "vit_dropout_bwd": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _U32, _P]),
     "vit_relu_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _P]),

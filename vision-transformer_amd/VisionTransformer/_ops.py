@@ -35,9 +35,10 @@ def _need_cuda(*ts):
 
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=1.0, beta=0.0, bias=None,
          act=ACT_NONE, aux=None, ldaux=0, res=None, ldres=0, res_rowmod=0, dropout_p=0.0, seed=0, split_k=1,
-         out_group=(0, 0), workspace=None, stream=None):
-    """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  Returns c."""
-    _need_cuda(a, b, c, bias, aux, res)
+         out_group=(0, 0), workspace=None, colsum_part=None, stream=None):
+    """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  `colsum_part` (f32, colsum_part_rows(m) x n)
+    receives per-256-row-block column sums of C as stored — finish with colsum_finish.  Returns c."""
+    _need_cuda(a, b, c, bias, aux, res, colsum_part)
     if a.dtype != b.dtype:
         raise TypeError("gemm: A and B dtypes differ")
     if bias is not None and bias.dtype != torch.float32:
@@ -58,13 +59,23 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=
     d.dropout_p, d.dropout_seed = dropout_p, seed & 0xFFFFFFFF
     d.split_k = split_k
     d.out_group_rows, d.out_group_stride = out_group
-    if split_k > 1:
-        need = _lib.load().vit_gemm_workspace_bytes(ctypes.byref(d))
+    if colsum_part is not None:
+        if colsum_part.dtype != torch.float32 or colsum_part.numel() < colsum_part_rows(m) * n:
+            raise ValueError("gemm: colsum_part must be float32 with >= ceil(m/256)*n elements")
+        d.colsum_part = colsum_part.data_ptr()
+    # split-K slabs (split_k > 1), or the slabs of the split-K tail of the last partial round of tiles
+    need = _lib.load().vit_gemm_workspace_bytes(ctypes.byref(d))
+    if need > 0:
         if workspace is None or workspace.numel() * workspace.element_size() < need:
             workspace = torch.empty(need // 4 + 1, dtype=torch.float32, device=c.device)
         d.workspace, d.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
     _lib.check(_lib.load().vit_gemm(ctypes.byref(d), _stream(stream)), "vit_gemm")
     return c
+
+
+def colsum_part_rows(m):
+    """Rows of a GEMM's colsum_part: one per 256-row block of C."""
+    return (m + 255) // 256
 
 
 def linear(x2d, w, bias=None, out_dtype=None, act=ACT_NONE, **kw):
@@ -104,16 +115,17 @@ def layernorm_bwd_parts(rows, cols):
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, drop_p=0.0, drop_seed=0,
-                  partial=None, stream=None):
+                  partial=None, osum=False, stream=None):
     """dx_out = LN_bwd(dy) (+ dres); drop_out = dropout_bwd(dx_out); returns partial [2, parts, cols] f32
-    (dgamma / dbeta per workgroup) — reduce with colsum."""
+    (dgamma / dbeta per workgroup) — [3, parts, cols] with `osum`: + the column sums of the stored gradient output
+    (drop_out when given, else dx_out), i.e. the bias gradient of the Linear it feeds.  Reduce with colsum_finish."""
     rows, cols = x.shape
     parts = layernorm_bwd_parts(rows, cols)
     if partial is None:
-        partial = torch.empty(2, parts, cols, dtype=torch.float32, device=x.device)
+        partial = torch.empty(3 if osum else 2, parts, cols, dtype=torch.float32, device=x.device)
     _lib.call("vit_layernorm_bwd", _ptr(dy), dy.stride(0), _ptr(x), x.stride(0), _ptr(gamma), _ptr(mean), _ptr(rstd),
-              _ptr(dres), _ptr(dx_out), _ptr(drop_out), drop_p, drop_seed & 0xFFFFFFFF, _ptr(partial), rows, cols,
-              dtype_code(x), _stream(stream))
+              _ptr(dres), _ptr(dx_out), _ptr(drop_out), drop_p, drop_seed & 0xFFFFFFFF, _ptr(partial), int(bool(osum)),
+              rows, cols, dtype_code(x), _stream(stream))
     return partial
 
 
@@ -148,6 +160,21 @@ def colsum(x, rows, cols, ldx, out, beta=0.0, workspace=None, stream=None):
     _lib.call("vit_colsum", _ptr(x), ldx, dtype_code(x), rows, cols, _ptr(out), beta, _ptr(workspace),
               _stream(stream))
     return out
+
+
+def colsum_finish(part, outs, beta=0.0, stream=None):
+    """outs[s] = beta * outs[s] + sum_p part[s][p] (fixed order) for s < len(outs) <= 3 — the second stage of the
+    column sums vit_gemm (colsum_part) and vit_layernorm_bwd produce.  part: [sets, nparts, cols] or [nparts, cols]."""
+    p3 = part if part.dim() == 3 else part.unsqueeze(0)
+    n = len(outs)
+    if not 1 <= n <= min(3, p3.shape[0]):
+        raise ValueError(f"colsum_finish: {n} outputs for {p3.shape[0]} partial sets")
+    for t in outs:
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != p3.shape[2]:
+            raise ValueError("colsum_finish: outputs must be contiguous float32 of length cols")
+    ptrs = [_ptr(t) for t in outs] + [None] * (3 - n)
+    _lib.call("vit_colsum_finish", _ptr(p3), p3.shape[1], p3.shape[2], n, *ptrs, beta, _stream(stream))
+    return outs
 
 
 def copy2d(src, lds, dst, ldd, rows, cols, group=(0, 0), beta=0.0, stream=None):

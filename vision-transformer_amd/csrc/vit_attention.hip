@@ -571,8 +571,8 @@ VIT_DEV bf16x8_t col_frag16(const bf16_t* img, int r0, int c0, int lane) {
 // into a swizzled [Tp][64] image: 1 KiB pieces of 8 rows, lane-linear destination, the chunk swizzle applied to
 // the source address; rows >= Tn are zero-filled by an out-of-range offset.
 VIT_DEV void dma_head_slice(__amdgpu_buffer_rsrc_t rs, int64_t row0, int64_t ld, int64_t col0, int Tn, int Tp,
-                            bf16_t* img, int wave, int lane) {
-  for (int pc = wave; pc < Tp / 8; pc += 8) {
+                            bf16_t* img, int wave, int lane, int nwaves = 8) {
+  for (int pc = wave; pc < Tp / 8; pc += nwaves) {
     const int r = pc * 8 + (lane >> 3);
     const int c = (lane & 7) ^ aswz(r);
     const uint32_t off = r < Tn ? (uint32_t)(2 * ((row0 + r) * ld + col0 + c * 8)) : 0x80000000u;
@@ -795,6 +795,105 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   store_rows64(Gs, Tp, Tn, dqkv + b * Tn * ld + 2 * D + h * HD, ld, tid, 512);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Fused forward for T <= 256 (ViT: T = 197): one workgroup per (image, head) with NKB = Tp/32 waves (Tp = T rounded up
+// to 32).  K and V of the head are LDS-DMA'd once into swizzled [Tp][64] images (rows >= T zero-filled); wave w owns
+// queries 32w..32w+31 (Q fragments straight from global) and walks the NKB key blocks with the online softmax of
+// attn_fwd_mfma (S^T = K Q^T: one query per lane column; P^T reused in registers as the B operand of O^T = V^T P^T).
+// Against attn_fwd_mfma (128-query workgroups over 64-key tiles) no all-padding query or key block is computed
+// (T = 197: 7 x 7 blocks of 32 instead of 8 x 8) and K/V leave HBM once per (image, head); at <= 64 KiB of LDS two
+// workgroups share a CU, so one's DMA prologue overlaps the other's loop.  O leaves registers as 16-B row pieces: a
+// permlane32 half swap pairs the two 8-B column groups a row is split over (cdna_hip_programming.md T21).
+// ---------------------------------------------------------------------------------------------------------------
+template <int NKB>
+__global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                           float* __restrict__ lse, int64_t Tn64, int64_t H,
+                                                           float scale) {
+  constexpr int Tp = NKB * 32;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * Tp * HD];
+  bf16_t* Ks = smem;
+  bf16_t* Vs = smem + Tp * HD;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Tn = (int)Tn64;
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * HD, ld = 3 * D;
+  const float c2 = scale * LOG2E;
+  {
+    const int64_t nb = gridDim.x / H;                  // host guarantees the tensor is < 2 GiB
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc_b(qkv, nb * Tn * ld * 2);
+    dma_head_slice(rq, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane, NKB);
+    dma_head_slice(rq, b * Tn, ld, 2 * D + h * HD, Tn, Tp, Vs, wave, lane, NKB);
+  }
+  const int q0 = wave * 32;
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = glb_frag(qkv + b * Tn * ld, ld, q0, Tn, h * HD, s, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x16 oacc[2] = {f32x16{}, f32x16{}};
+  float m_run = -INFINITY, l_run = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < Tp; kb += 32) {
+    f32x16 sacc = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) sacc = mfma32(row_frag(Ks, kb, s, lane), qf[s], sacc);
+    float x[16];
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      x[r] = kb + acc_row(r, hf) < Tn ? sacc[r] * c2 : -INFINITY;
+      mloc = fmaxf(mloc, x[r]);
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      x[r] = exp2f(x[r] - m_new);
+      psum += x[r];
+    }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    oacc[0] *= alpha;
+    oacc[1] *= alpha;
+    const bf16x8_t pb0 = pack8(x), pb1 = pack8(x + 8);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      oacc[db] = mfma32(tr_frag(Vs, kb, db, lane), pb0, oacc[db]);
+      oacc[db] = mfma32(tr_frag(Vs, kb + 16, db, lane), pb1, oacc[db]);
+    }
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.0f / l_tot;
+  const int q = q0 + (lane & 31);
+  // lane (q, hf) holds O[q][8k + 4hf .. 8k + 4hf + 3] in group k = 4db + g; one permlane32 swap per dword pairs groups
+  // (k, k+1) into 16 contiguous bytes per lane: columns 8k..8k+7 on lanes < 32, 8k+8..8k+15 on lanes >= 32
+  uint32_t pk[8][2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = 4 * db + g;
+      pk[k][0] = (uint32_t)f2bf(oacc[db][4 * g] * inv) | ((uint32_t)f2bf(oacc[db][4 * g + 1] * inv) << 16);
+      pk[k][1] = (uint32_t)f2bf(oacc[db][4 * g + 2] * inv) | ((uint32_t)f2bf(oacc[db][4 * g + 3] * inv) << 16);
+    }
+  bf16_t* orow = o + (b * Tn + q) * D + h * HD + 8 * hf;
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(pk[k][w2], pk[k + 1][w2], false, false);
+      pk[k][w2] = sw[0];
+      pk[k + 1][w2] = sw[1];
+    }
+    if (q < Tn) *reinterpret_cast<uint4*>(orow + 8 * k) = make_uint4(pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]);
+  }
+  if (q < Tn && hf == 0) lse[bh * Tn + q] = (m_run + log2f(l_tot)) / LOG2E;
+}
+
 bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }
 
 }  // namespace
@@ -805,8 +904,23 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* lse, float* probs, 
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && probs == nullptr) {
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
-    dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
-    attn_fwd_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, scale);
+    if (T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_FWD_SPLIT")) {
+#define FWD(NK) attn_fwd_fused<NK><<<(unsigned)(B * H), NK * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, scale)
+      switch ((int)((T + 31) / 32)) {
+        case 1: FWD(1); break;
+        case 2: FWD(2); break;
+        case 3: FWD(3); break;
+        case 4: FWD(4); break;
+        case 5: FWD(5); break;
+        case 6: FWD(6); break;
+        case 7: FWD(7); break;
+        default: FWD(8); break;
+      }
+#undef FWD
+    } else {
+      dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
+      attn_fwd_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, scale);
+    }
   } else {
     VIT_REQUIRE(T <= GA_TMAX && hd <= GA_HDMAX, "vit_attn_fwd(generic): T<=%d, hd<=%d", GA_TMAX, GA_HDMAX);
     dim3 grid((unsigned)((T + 3) / 4), (unsigned)(B * H));

@@ -90,6 +90,9 @@ VIT_DEV float gelu_erf_grad(float x) {
 namespace vit {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// part[chunk][cols] = column sums of x rows [chunk*rows_per_chunk, ...) (vit_misc.hip; stage 1 of vit_colsum)
+void colsum_parts_launch(const void* x, int64_t ldx, int dtype, int64_t rows, int64_t cols, int64_t rows_per_chunk,
+                         float* part, hipStream_t s);
 }  // namespace vit
 
 #define VIT_REQUIRE(cond, ...)                 \

@@ -35,6 +35,8 @@ struct EpiParams {
   int use_drop;
   int64_t grp, grp_stride;
   int vec;  // all row strides/pointers allow 4-wide vector access
+  float* csum;     // v4 fast epilogues: per-tile column sums of C as stored -> csum[tile row][n] (colsum_part)
+  int64_t row0;    // global row of local row 0 (split-K tail launch): dropout indices use the global row
 };
 
 struct GemmArgs {
@@ -87,7 +89,7 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
       for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
     }
     if (e.use_drop) {
-      const uint32_t base = (uint32_t)(i * e.n + j);
+      const uint32_t base = (uint32_t)((i + e.row0) * e.n + j);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         v[r] = vit_hash_u32(e.seed, base + r) >= e.drop_thr ? v[r] * e.drop_scale : 0.f;
@@ -111,7 +113,7 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
       if (e.act == VIT_ACT_RELU) x = fmaxf(x, 0.f);
       else if (e.act == VIT_ACT_GELU) x = gelu_erf(x);
       if (e.aux) x = ld_any(e.aux, e.aux_dtype, i * e.ldaux + jj) > 0.f ? x : 0.f;
-      if (e.use_drop) x = vit_hash_u32(e.seed, (uint32_t)(i * e.n + jj)) >= e.drop_thr ? x * e.drop_scale : 0.f;
+      if (e.use_drop) x = vit_hash_u32(e.seed, (uint32_t)((i + e.row0) * e.n + jj)) >= e.drop_thr ? x * e.drop_scale : 0.f;
       if (e.res) x += ld_any(e.res, e.res_dtype, rrow * e.ldres + jj);
       st1<TO>(cp + r, x);
     }
@@ -547,7 +549,7 @@ VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_
   }
   if (KIND == EPI_BDR) {
     if (e.use_drop) {
-      const uint32_t base = (uint32_t)(i * e.n + j);
+      const uint32_t base = (uint32_t)((i + e.row0) * e.n + j);
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = vit_hash_u32(e.seed, base + r) >= e.drop_thr ? v[r] * e.drop_scale : 0.f;
     }
@@ -751,6 +753,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   // second-operand rows of both passes, in flight before the LDS round trip (see v4_has_pre)
   uint2 pre[2][16];
   const bool has_pre = v4_has_pre<KIND>(e);
+  // fused column sums of C as stored (the bias gradient of the Linear whose input gradient C is)
+  const bool cs_on = (KIND == EPI_PLAIN || KIND == EPI_BIAS_ACT || KIND == EPI_AUX || KIND == EPI_BDR) &&
+                     e.csum != nullptr;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
   if (has_pre) {
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
@@ -781,8 +787,24 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
       if (v[0] != 1234.5f) continue;
 #endif
       v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
+      if (cs_on && i < e.m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[r] += sizeof(TO) == 2 ? bf2f(f2bf(v[r])) : v[r];
+      }
     }
     if (mh == 0) __syncthreads();
+  }
+  if (cs_on) {
+    // per-lane sums of the wave's 32 rows -> LDS -> the 8 wave sums added in wave order: one row of csum per tile
+    __syncthreads();
+    *reinterpret_cast<f32x4*>(ep + wave * 256 + 4 * lane) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    __syncthreads();
+    if (tid < 256 && j0 + tid < e.n) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) sum += ep[w8 * 256 + tid];
+      e.csum[tm * e.n + j0 + tid] = sum;
+    }
   }
 #endif
 }
@@ -888,11 +910,35 @@ int gemm_impl(int64_t m, int64_t n) {
   return (m >= 256 && n >= 256) ? 4 : 2;
 }
 
+// Split-K tail of a v4 GEMM (see vit_gemm): the K split for the tile rows past the last whole round of the 256 CUs,
+// or 1 when that last round would be more than half full (or the kernel / epilogue does not allow it).
+// *m_main = the rows of the whole rounds.
+int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
+  *m_main = d->m;
+  if (d->split_k > 1 || d->in_dtype != VIT_BF16 || d->k % BK != 0 || d->m <= 0 || d->n <= 0) return 1;
+  if (gemm_impl(d->m, d->n) != 4 || d->out_group_rows != 0 || d->res_rowmod != 0) return 1;
+  const char* v = getenv("VIT_GEMM_TAIL");
+  if (v && v[0] == '0') return 1;
+  const int64_t tn = (d->n + 255) / 256, tm = (d->m + 255) / 256, nkt = d->k / BK;
+  const int64_t rounds = tm * tn / 256;
+  if (rounds < 1 || nkt < 8) return 1;
+  const int64_t mr = rounds * 256 / tn;                    // tile rows that fill whole rounds
+  const int64_t tail = (tm - mr) * tn;                     // tiles of the last, partial round
+  if (tail <= 0 || 2 * tail > 256) return 1;
+  const int64_t sk = std::min<int64_t>(std::min<int64_t>(256 / tail, nkt / 4), 8);
+  if (sk < 2) return 1;
+  *m_main = mr * 256;
+  return (int)sk;
+}
+
 }  // namespace
 
 extern "C" int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d) {
-  if (!d || d->split_k <= 1) return 0;
-  return (int64_t)d->split_k * d->m * d->n * (int64_t)sizeof(float);
+  if (!d) return 0;
+  if (d->split_k > 1) return (int64_t)d->split_k * d->m * d->n * (int64_t)sizeof(float);
+  int64_t m_main = 0;
+  const int sk = tail_split(d, &m_main);
+  return sk > 1 ? (int64_t)sk * (d->m - m_main) * d->n * (int64_t)sizeof(float) : 0;
 }
 
 extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dtype) {
@@ -910,9 +956,12 @@ extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dty
   return (int)std::max<int64_t>(1, s);
 }
 
-extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
+// One GEMM launch (+ the split-K reduce, + the column-sum pass when it is not fused); row0 = global row of local
+// row 0 (dropout indices).
+static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
   VIT_REQUIRE(d != nullptr, "vit_gemm: null descriptor");
   VIT_REQUIRE(d->a && d->b && d->c, "vit_gemm: null operand pointer");
+  VIT_REQUIRE(!d->colsum_part || d->out_group_rows == 0, "vit_gemm: colsum_part needs ungrouped output rows");
   VIT_REQUIRE(d->m > 0 && d->n > 0 && d->k > 0, "vit_gemm: bad shape m=%lld n=%lld k=%lld", (long long)d->m,
               (long long)d->n, (long long)d->k);
   VIT_REQUIRE(d->in_dtype == VIT_F32 || d->in_dtype == VIT_BF16, "vit_gemm: bad in_dtype %d", d->in_dtype);
@@ -936,6 +985,9 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
   e.drop_scale = e.use_drop ? 1.0f / (1.0f - d->dropout_p) : 1.0f;
   e.grp = d->out_group_rows;
   e.grp_stride = d->out_group_stride;
+  e.csum = nullptr;
+  e.row0 = row0;
+  bool cs_fused = false;
   e.vec = (d->n % 4 == 0) && (d->ldc % 4 == 0) && aligned(d->c, 16) && aligned(d->bias, 16) &&
           (!d->aux || (d->ldaux % 4 == 0 && aligned(d->aux, 16))) &&
           (!d->res || (d->ldres % 4 == 0 && aligned(d->res, 16)));
@@ -987,16 +1039,24 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
       kind = EPI_BDR;
     const char* dk = getenv("VIT_GEMM_EPI_GENERAL");      // A/B switch: force the general epilogue
     if (dk && dk[0] == '1' && kind != EPI_SLAB) kind = EPI_GENERAL;
+    // the v4 epilogue instantiation that runs (fast kinds exist for bf16 output and these operand layouts only)
+    int launched = EPI_GENERAL;
+    if (kind == EPI_SLAB) launched = EPI_SLAB;
+    else if (out_bf && kind == EPI_PLAIN) launched = EPI_PLAIN;
+    else if (out_bf && akc && bkc && (kind == EPI_BIAS_ACT || kind == EPI_BDR)) launched = kind;
+    else if (out_bf && akc && !bkc && kind == EPI_AUX) launched = EPI_AUX;
+    cs_fused = v4 && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
+    e.csum = cs_fused ? d->colsum_part : nullptr;
 #define V4(AK, BKK, TO, KIND) gemm_bf16_v4<AK, BKK, TO, KIND><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes)
 #define LAUNCH_BF(AK, BKK)                                                                                     \
   do {                                                                                                         \
     if (v4) {                                                                                                  \
-      if (kind == EPI_SLAB) V4(AK, BKK, float, EPI_SLAB);                                                      \
+      if (launched == EPI_SLAB) V4(AK, BKK, float, EPI_SLAB);                                                  \
       else if (!out_bf) V4(AK, BKK, float, EPI_GENERAL);                                                       \
-      else if (kind == EPI_PLAIN) V4(AK, BKK, bf16_t, EPI_PLAIN);                                              \
-      else if (AK && BKK && kind == EPI_BIAS_ACT) V4(AK, BKK, bf16_t, EPI_BIAS_ACT);                           \
-      else if (AK && BKK && kind == EPI_BDR) V4(AK, BKK, bf16_t, EPI_BDR);                                     \
-      else if (AK && !BKK && kind == EPI_AUX) V4(AK, BKK, bf16_t, EPI_AUX);                                    \
+      else if (launched == EPI_PLAIN) V4(AK, BKK, bf16_t, EPI_PLAIN);                                          \
+      else if (AK && BKK && launched == EPI_BIAS_ACT) V4(AK, BKK, bf16_t, EPI_BIAS_ACT);                       \
+      else if (AK && BKK && launched == EPI_BDR) V4(AK, BKK, bf16_t, EPI_BDR);                                 \
+      else if (AK && !BKK && launched == EPI_AUX) V4(AK, BKK, bf16_t, EPI_AUX);                                \
       else V4(AK, BKK, bf16_t, EPI_GENERAL);                                                                   \
     } else if (v2) {                                                                                           \
       if (out_bf && split == 1) gemm_bf16_v2<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);     \
@@ -1035,5 +1095,35 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     if (out_bf) splitk_reduce_kernel<bf16_t><<<(unsigned)blocks, 256, 0, s>>>(g.ws, d->m, d->n, split, e);
     else splitk_reduce_kernel<float><<<(unsigned)blocks, 256, 0, s>>>(g.ws, d->m, d->n, split, e);
   }
+  if (d->colsum_part && !cs_fused)
+    vit::colsum_parts_launch(d->c, d->ldc, d->out_dtype, d->m, d->n, 256, d->colsum_part, s);
   return vit::check_launch("vit_gemm");
+}
+
+// When the 256x256 tiles leave the last round of the 256 CUs at most half full (tail_split), the whole rounds run as
+// one launch and the remaining tile rows run split-K over the otherwise idle CUs: fp32 slabs in the caller's
+// workspace, then the deterministic reduce applies the same epilogue (dropout indices keep the global row; column
+// sums land in the same colsum_part rows).  Without a large enough workspace the GEMM runs unsplit.
+extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
+  VIT_REQUIRE(d != nullptr, "vit_gemm: null descriptor");
+  int64_t m_main = 0;
+  const int sk = tail_split(d, &m_main);
+  if (sk > 1 && d->workspace && d->workspace_bytes >= vit_gemm_workspace_bytes(d)) {
+    vit_gemm_desc dm = *d;
+    dm.m = m_main;
+    const int rc = gemm_run(&dm, 0, stream);
+    if (rc) return rc;
+    auto esz = [](int32_t t) { return t == VIT_BF16 ? (int64_t)2 : (int64_t)4; };
+    const int64_t r = m_main;
+    vit_gemm_desc dt = *d;
+    dt.a = (const char*)d->a + (d->a_kcontig ? r * d->lda : r) * 2;
+    dt.c = (char*)d->c + r * d->ldc * esz(d->out_dtype);
+    if (d->aux) dt.aux = (const char*)d->aux + r * d->ldaux * esz(d->aux_dtype);
+    if (d->res) dt.res = (const char*)d->res + r * d->ldres * esz(d->res_dtype);
+    if (d->colsum_part) dt.colsum_part = d->colsum_part + (r / 256) * d->n;
+    dt.m = d->m - r;
+    dt.split_k = sk;
+    return gemm_run(&dt, r, stream);
+  }
+  return gemm_run(d, 0, stream);
 }

@@ -108,12 +108,18 @@ __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ x, in
 
 // Stage 2: 64 columns per block; 16 waves stride over the chunk partials (wave w sums chunks w, w+16, ...), then the
 // 16 wave sums are added in wave order through LDS -> deterministic for a given (rows, cols).
+// blockIdx.y selects one of up to 3 independent sets: part + set*nchunks*cols -> outs.p[set] (vit_colsum_finish).
 constexpr int CS2_WAVES = 16;
+struct OutSet {
+  float* p[3];
+};
 __global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2(const float* __restrict__ part, int64_t nchunks,
-                                                                int64_t cols, float* __restrict__ out, float beta) {
+                                                                int64_t cols, OutSet outs, float beta) {
   __shared__ float red[CS2_WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  part += (int64_t)blockIdx.y * nchunks * cols;
+  float* __restrict__ out = blockIdx.y == 0 ? outs.p[0] : (blockIdx.y == 1 ? outs.p[1] : outs.p[2]);
   float s0 = 0.f, s1 = 0.f;
   if (c < cols) {
     int64_t k = w;
@@ -295,6 +301,19 @@ extern "C" int vit_embed_cls(const float* cls, const float* pos, void* x0, int32
   return vit::check_launch("vit_embed_cls");
 }
 
+namespace vit {
+void colsum_parts_launch(const void* x, int64_t ldx, int dtype, int64_t rows, int64_t cols, int64_t rows_per_chunk,
+                         float* part, hipStream_t s) {
+  const int64_t ch = (rows + rows_per_chunk - 1) / rows_per_chunk;
+  const int vec = (cols % 4 == 0) && (ldx % 4 == 0) && (((uintptr_t)x) % 16 == 0);
+  dim3 g1((unsigned)((cols + 255) / 256), (unsigned)ch);
+  if (dtype == VIT_BF16)
+    colsum_stage1<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)x, ldx, rows, cols, rows_per_chunk, part, vec);
+  else
+    colsum_stage1<float><<<g1, 256, 0, s>>>((const float*)x, ldx, rows, cols, rows_per_chunk, part, vec);
+}
+}  // namespace vit
+
 extern "C" int64_t vit_colsum_workspace_bytes(int64_t rows, int64_t cols) {
   return colsum_chunks(rows, cols) * cols * (int64_t)sizeof(float);
 }
@@ -311,8 +330,19 @@ extern "C" int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t row
     colsum_stage1<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
   else
     colsum_stage1<float><<<g1, 256, 0, s>>>((const float*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
-  colsum_stage2<<<(unsigned)((cols + 63) / 64), 64 * CS2_WAVES, 0, s>>>((const float*)workspace, ch, cols, out, beta);
+  OutSet outs{{out, nullptr, nullptr}};
+  colsum_stage2<<<(unsigned)((cols + 63) / 64), 64 * CS2_WAVES, 0, s>>>((const float*)workspace, ch, cols, outs, beta);
   return vit::check_launch("vit_colsum");
+}
+
+extern "C" int vit_colsum_finish(const float* part, int64_t nparts, int64_t cols, int32_t nsets, float* out0,
+                                 float* out1, float* out2, float beta, void* stream) {
+  VIT_REQUIRE(part && nparts > 0 && cols > 0 && nsets >= 1 && nsets <= 3, "vit_colsum_finish: bad arguments");
+  OutSet outs{{out0, out1, out2}};
+  for (int i = 0; i < nsets; ++i) VIT_REQUIRE(outs.p[i] != nullptr, "vit_colsum_finish: output %d is NULL", i);
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)nsets);
+  colsum_stage2<<<grid, 64 * CS2_WAVES, 0, VIT_STREAM(stream)>>>(part, nparts, cols, outs, beta);
+  return vit::check_launch("vit_colsum_finish");
 }
 
 extern "C" int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,

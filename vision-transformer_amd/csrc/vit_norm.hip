@@ -63,50 +63,59 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, in
   }
 }
 
+// the value of v as stored in T (bf16 rounds to nearest even)
+template <class T> VIT_DEV float as_stored(float v) { return sizeof(T) == 2 ? bf2f(f2bf(v)) : v; }
+
 template <class T, int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
                                                      int64_t ldx, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const T* __restrict__ dres, T* __restrict__ dx_out,
                                                      T* __restrict__ drop_out, uint32_t drop_thr, float drop_scale,
-                                                     uint32_t drop_seed, float* __restrict__ partial, int64_t parts,
-                                                     int64_t rows, int64_t cols) {
-  __shared__ float red[2][256 * NV];
+                                                     uint32_t drop_seed, float* __restrict__ partial, int osum,
+                                                     int64_t parts, int64_t rows, int64_t cols) {
+  __shared__ float red[3][256 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t rows_per_part = (rows + parts - 1) / parts;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_part, r1 = min(rows, r0 + rows_per_part);
-  float dg[NV][4], db[NV][4], gm[NV][4];
+  float dg[NV][4], db[NV][4], os[NV][4], gm[NV][4];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int64_t c = ((int64_t)k * 64 + lane) * 4;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dg[k][r] = db[k][r] = 0.f;
+    for (int r = 0; r < 4; ++r) dg[k][r] = db[k][r] = os[k][r] = 0.f;
     if (c < cols) ld4<float>(gamma + c, gm[k]);
     else gm[k][0] = gm[k][1] = gm[k][2] = gm[k][3] = 0.f;
   }
   for (int64_t row = r0 + w; row < r1; row += 4) {
     const float mu = mean[row], rs = rstd[row];
-    float xh[NV][4], g[NV][4];
-    float sa = 0.f, sb = 0.f;
+    // every load of the row (x, dy, residual gradient) is issued before the first reduction: one memory round trip
+    // per row instead of two
+    float xv[NV][4], dv[NV][4], rv[NV][4];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int64_t c = ((int64_t)k * 64 + lane) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xv[k][r] = dv[k][r] = rv[k][r] = 0.f;
       if (c < cols) {
-        float xv[4], dv[4];
-        ld4<T>(x + row * ldx + c, xv);
-        ld4<T>(dy + row * lddy + c, dv);
+        ld4<T>(x + row * ldx + c, xv[k]);
+        ld4<T>(dy + row * lddy + c, dv[k]);
+        if (dres) ld4<T>(dres + row * cols + c, rv[k]);
+      }
+    }
+    float sa = 0.f, sb = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          xh[k][r] = (xv[r] - mu) * rs;
-          g[k][r] = dv[r] * gm[k][r];
-          sa += g[k][r];
-          sb += g[k][r] * xh[k][r];
-          dg[k][r] += dv[r] * xh[k][r];
-          db[k][r] += dv[r];
-        }
-      } else {
+    for (int k = 0; k < NV; ++k) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xh[k][r] = g[k][r] = 0.f;
+      for (int r = 0; r < 4; ++r) {          // columns past `cols` have dv = gm = 0: they add exact zeros
+        const float xh = (xv[k][r] - mu) * rs;
+        const float g = dv[k][r] * gm[k][r];
+        sa += g;
+        sb += g * xh;
+        dg[k][r] += dv[k][r] * xh;
+        db[k][r] += dv[k][r];
+        xv[k][r] = xh;
+        dv[k][r] = g;
       }
     }
     const float a = wave_sum(sa) / (float)cols;
@@ -117,30 +126,28 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
       if (c < cols) {
         float o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = rs * (g[k][r] - a - xh[k][r] * b);
-        if (dres) {
-          float d[4];
-          ld4<T>(dres + row * cols + c, d);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] += d[r];
-        }
+        for (int r = 0; r < 4; ++r) o[r] = rs * (dv[k][r] - a - xv[k][r] * b) + rv[k][r];
         st4<T>(dx_out + row * cols + c, o);
         if (drop_out) {
+          // drop the value as stored (rounded), matching a separate dropout-backward pass over dx_out
           const uint32_t base = (uint32_t)(row * cols + c);
           float dd[4];
-          if (sizeof(T) == 2) {
-            // drop the value as stored (rounded), matching a separate dropout-backward pass over dx_out
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = bf2f(f2bf(o[r]));
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? o[r] * drop_scale : 0.f;
+          for (int r = 0; r < 4; ++r)
+            dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? as_stored<T>(o[r]) * drop_scale : 0.f;
           st4<T>(drop_out + row * cols + c, dd);
+          if (osum) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) os[k][r] += as_stored<T>(dd[r]);
+          }
+        } else if (osum) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) os[k][r] += as_stored<T>(o[r]);
         }
       }
     }
   }
-  // per-block dgamma/dbeta partial: waves add into LDS in a fixed order (0, 1, 2, 3) -> bitwise reproducible
+  // per-block partial sums: waves add into LDS in a fixed order (0, 1, 2, 3) -> bitwise reproducible
   for (int turn = 0; turn < 4; ++turn) {
     if (w == turn) {
 #pragma unroll
@@ -151,19 +158,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
           if (turn == 0) {
             red[0][cc] = dg[k][r];
             red[1][cc] = db[k][r];
+            red[2][cc] = os[k][r];
           } else {
             red[0][cc] += dg[k][r];
             red[1][cc] += db[k][r];
+            red[2][cc] += os[k][r];
           }
         }
       }
     }
     __syncthreads();
   }
-  for (int64_t c = threadIdx.x; c < cols; c += 256) {
-    partial[(int64_t)blockIdx.x * cols + c] = red[0][c];
-    partial[(parts + blockIdx.x) * cols + c] = red[1][c];
-  }
+  const int nset = osum ? 3 : 2;
+  for (int64_t c = threadIdx.x; c < cols; c += 256)
+    for (int s = 0; s < nset; ++s) partial[(s * parts + blockIdx.x) * cols + c] = red[s][c];
 }
 
 template <int NV, class T>
@@ -217,8 +225,8 @@ extern "C" int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma,
 
 extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
                                  const float* mean, const float* rstd, const void* dres, void* dx_out,
-                                 void* drop_out, float drop_p, uint32_t drop_seed, float* partial, int64_t rows,
-                                 int64_t cols, int32_t dtype, void* stream) {
+                                 void* drop_out, float drop_p, uint32_t drop_seed, float* partial, int32_t osum,
+                                 int64_t rows, int64_t cols, int32_t dtype, void* stream) {
   VIT_REQUIRE(dy && x && gamma && mean && rstd && dx_out && partial && rows > 0 && cols > 0,
               "vit_layernorm_bwd: bad arguments");
   VIT_REQUIRE(cols % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0, "vit_layernorm_bwd: cols/ld must be multiples of 4");
@@ -233,14 +241,14 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
 #define CALLB(NV)                                                                                               \
   ln_bwd_kernel<bf16_t, NV><<<(unsigned)parts, 256, 0, s>>>(                                                    \
       (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
-      (bf16_t*)drop_out, thr, scale, drop_seed, partial, parts, rows, cols)
+      (bf16_t*)drop_out, thr, scale, drop_seed, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLB)
 #undef CALLB
   } else {
 #define CALLF(NV)                                                                                            \
   ln_bwd_kernel<float, NV><<<(unsigned)parts, 256, 0, s>>>(                                                  \
       (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out,   \
-      (float*)drop_out, thr, scale, drop_seed, partial, parts, rows, cols)
+      (float*)drop_out, thr, scale, drop_seed, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLF)
 #undef CALLF
   }
