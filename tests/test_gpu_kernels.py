@@ -253,15 +253,15 @@ def test_gemm_colsum_part(variant):
 @pytest.mark.parametrize("variant", ["plain", "bias_relu", "aux", "bias_drop_res"])
 def test_gemm_split_k_tail(monkeypatch, variant):
     """A v4 GEMM whose 256x256 tiles leave the last round of the 256 CUs at most half full runs the remaining tile
-    rows split-K (M = 23140, N = 768: 91 x 3 tiles = 85 tile rows in whole rounds + 6 tile rows split 3 ways).
+    rows split-K (M = 23140, N = 768, K = 2304: 91 x 3 tiles = 85 tile rows in whole rounds + 6 tile rows split 8 ways).
     Integer data: outputs and fused column sums equal the unsplit kernel's bit for bit, dropout masks included."""
     import ctypes
     from VisionTransformer import _lib
     g = torch.Generator().manual_seed(5)
-    M, N, K = 90 * 256 + 100, 768, 768
+    M, N, K = 90 * 256 + 100, 768, 2304
     d = _lib.GemmDesc()
     d.m, d.n, d.k, d.a_kcontig, d.b_kcontig, d.in_dtype, d.out_dtype = M, N, K, 1, 1, 1, 1
-    assert _lib.load().vit_gemm_workspace_bytes(ctypes.byref(d)) == 3 * (M - 85 * 256) * N * 4
+    assert _lib.load().vit_gemm_workspace_bytes(ctypes.byref(d)) == 8 * (M - 85 * 256) * N * 4
     a = _ints((M, K), gen=g)
     b = _ints((N, K), gen=g)
     bias = _ints((N,), gen=g, dtype=torch.float32)

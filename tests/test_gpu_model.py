@@ -263,7 +263,7 @@ def test_vit_base_224_bf16_full_size_properties():
 
 
 def test_side_stream_weight_gradients_bitwise_equal():
-    """Weight gradients on the side stream (default) equal the in-order schedule bit for bit (train mode, bf16)."""
+    """Weight gradients on the side stream (VIT_CONCURRENT_WGRAD=1) equal the in-order schedule bit for bit."""
     ocfg = O.make_config("micro", img=64, batch=4, blocks=2)
     ocfg.embedding_size, ocfg.num_heads = 128, 2
     st = O.init_state(ocfg, seed=4)

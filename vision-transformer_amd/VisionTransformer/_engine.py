@@ -104,8 +104,9 @@ class Engine:
         self._ver_sig = None
         self.stats = {"packs": 0}
         self.profile_hook = None          # callable(name, phase) around named launches (bench.py HIP events)
-        # weight-gradient GEMMs on a side stream (VIT_CONCURRENT_WGRAD=0: in order on the current stream)
-        self.concurrent_wgrad = os.environ.get("VIT_CONCURRENT_WGRAD", "1") != "0"
+        # weight-gradient GEMMs on a side stream (VIT_CONCURRENT_WGRAD=1).  Off by default: measured on ViT-B/16
+        # B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms/step).
+        self.concurrent_wgrad = os.environ.get("VIT_CONCURRENT_WGRAD", "0") == "1"
         self._wstream = None
         self._wws = None
 

@@ -921,7 +921,9 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
   if (v && v[0] == '0') return 1;
   const int64_t tn = (d->n + 255) / 256, tm = (d->m + 255) / 256, nkt = d->k / BK;
   const int64_t rounds = tm * tn / 256;
-  if (rounds < 1 || nkt < 8) return 1;
+  // measured (ViT-B/16 B=256, N = 768): a net win at K >= 2304, a loss at K = 768, where a tile's k-loop is short
+  // against the slab round trip
+  if (rounds < 1 || nkt < 32) return 1;
   const int64_t mr = rounds * 256 / tn;                    // tile rows that fill whole rounds
   const int64_t tail = (tm - mr) * tn;                     // tiles of the last, partial round
   if (tail <= 0 || 2 * tail > 256) return 1;
