@@ -44,6 +44,8 @@ struct GemmArgs {
   const void* b;
   int64_t lda, ldb, M, N, K;
   int64_t tiles_n;
+  int64_t tiles_m, group_m;  // v4: tile order inside an XCD's contiguous range = groups of group_m tile rows,
+                             // column-major inside a group (group_m = 1: row-major)
   int64_t kt_per_split;  // k-tiles per split
   float* ws;             // split-K slabs [split][M][N]
 };
@@ -592,9 +594,24 @@ VIT_DEV void dma_half(__amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[2], uint3
         rs, (__attribute__((address_space(3))) void*)(half + (wave * 2 + i) * 512), 16, off[i], soff, 0, 0);
 }
 
-// vmcnt for phase f: DMA stages younger than s = f+2 that exist may stay in flight (2 instructions each)
+// LDS ring of the v4 k-loop: V4_SLOTS half-tile images (16 KiB each); stage s (k-tile s/4, half A0/B0/B1/A1) lands in
+// slot s % V4_SLOTS and is issued V4_LEAD phases before the phase that first needs it retired.  A slot is
+// re-staged (stage s + SLOTS, issued in phase s + SLOTS - LEAD) >= 2 phases after stage s's last read (phase <= s),
+// so LEAD <= SLOTS - 2.  Measured (tools/r2g.sh, ViT-B/16 shapes): 10 slots / lead 8 (160 KiB, 6 stages in flight
+// across every barrier) and 10 / 7 are no faster than 8 / 6 (4 stages in flight), so the default stays 8 / 6.
+#ifndef V4_SLOTS
+#define V4_SLOTS 8
+#endif
+#ifndef V4_LEAD
+#define V4_LEAD (V4_SLOTS - 2)
+#endif
+static_assert(V4_LEAD <= V4_SLOTS - 2 && V4_LEAD >= 4 && V4_LEAD <= 8, "v4 ring: 4 <= LEAD <= SLOTS - 2, LEAD <= 8");
+
+// vmcnt for phase f: the `left` DMA stages younger than s = f+2 that exist may stay in flight (2 instructions each)
 VIT_DEV void wait_stage_retired(int left) {
-  if (left >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  if (left >= 6) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (left == 5) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if (left == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if (left == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if (left == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if (left == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -631,14 +648,24 @@ VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const
 
 template <bool AKC, bool BKC, class TO, int KIND>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem4[2 * 4 * HALF];
+  __shared__ __attribute__((aligned(16))) bf16_t smem4[V4_SLOTS * HALF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int64_t nwg = gridDim.x, orig = blockIdx.x;
   const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
   const int64_t bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int64_t tm = bid / g.tiles_n, tn = bid % g.tiles_n;
+  int64_t tm, tn;
+  if (g.group_m > 1) {
+    // L2 locality: the ~32 tiles an XCD runs at once span group_m A panels x 32/group_m B panels
+    const int64_t span = g.group_m * g.tiles_n, first = (bid / span) * g.group_m;
+    const int64_t gs = min(g.tiles_m - first, g.group_m), in = bid % span;
+    tm = first + in % gs;
+    tn = in / gs;
+  } else {
+    tm = bid / g.tiles_n;
+    tn = bid % g.tiles_n;
+  }
   const int64_t i0 = tm * 256, j0 = tn * 256;
   const int64_t nkt = g.K / BK;
   const int64_t kt0 = (int64_t)blockIdx.y * g.kt_per_split;
@@ -653,16 +680,17 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   dma_offsets4<BKC>(g.ldb, g.N, j0, kt0 * BK, wave, lane, ob0);
   dma_offsets4<BKC>(g.ldb, g.N, j0 + 128, kt0 * BK, wave, lane, ob1);
 
-  // stage s -> (k-tile s>>2, half order A0, B0, B1, A1); LDS half index: A0 0, A1 1, B0 2, B1 3
+  // stage s -> (k-tile s>>2, half order A0, B0, B1, A1) in LDS slot s % V4_SLOTS
+#define V4_SLOT(S) (smem4 + ((S) % V4_SLOTS) * HALF)
 #define V4_STAGE(S)                                                                              \
   do {                                                                                           \
     const int s_ = (S), u_ = s_ >> 2;                                                            \
-    bf16_t* buf_ = smem4 + (u_ & 1) * 4 * HALF;                                                  \
+    bf16_t* slot_ = V4_SLOT(s_);                                                                 \
     switch (s_ & 3) {                                                                            \
-      case 0: dma_half(ra, oa0, (uint32_t)u_ * sa, buf_, wave); break;                           \
-      case 1: dma_half(rb, ob0, (uint32_t)u_ * sb, buf_ + 2 * HALF, wave); break;                \
-      case 2: dma_half(rb, ob1, (uint32_t)u_ * sb, buf_ + 3 * HALF, wave); break;                \
-      default: dma_half(ra, oa1, (uint32_t)u_ * sa, buf_ + HALF, wave); break;                   \
+      case 0: dma_half(ra, oa0, (uint32_t)u_ * sa, slot_, wave); break;                          \
+      case 1: dma_half(rb, ob0, (uint32_t)u_ * sb, slot_, wave); break;                          \
+      case 2: dma_half(rb, ob1, (uint32_t)u_ * sb, slot_, wave); break;                          \
+      default: dma_half(ra, oa1, (uint32_t)u_ * sa, slot_, wave); break;                         \
     }                                                                                            \
   } while (0)
 
@@ -677,29 +705,28 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
         for (int y = 0; y < 2; ++y) acc[a][b][x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nstage = 4 * nk;
-  // prologue: stages 0..5; retire stages 0 and 1 (k-tile 0's A_0, B_0) before the common barrier
-  for (int s = 0; s < 6 && s < nstage; ++s) V4_STAGE(s);
-  if (nstage > 0) wait_stage_retired(min(5, nstage - 1) - 1);
+  // prologue: stages 0..LEAD-1; retire stages 0 and 1 (k-tile 0's A_0, B_0) before the common barrier
+  for (int s = 0; s < V4_LEAD && s < nstage; ++s) V4_STAGE(s);
+  if (nstage > 0) wait_stage_retired(min(V4_LEAD - 1, nstage - 1) - 1);
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();              // group 1 runs one barrier behind group 0
 
   bf16x8_t af[4][2], b0f[2][2], b1f[2][2];
   for (int t = 0; t < nk; ++t) {
-    const bf16_t* buf = smem4 + (t & 1) * 4 * HALF;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * t + r;
       if (r == 0) {
-        read_a4<AKC, BKC>(buf, wr, lane, af);
-        read_b4<BKC>(buf + 2 * HALF, wc, lane, b0f);
+        read_a4<AKC, BKC>(V4_SLOT(4 * t), wr, lane, af);
+        read_b4<BKC>(V4_SLOT(4 * t + 1), wc, lane, b0f);
       } else if (r == 1) {
-        read_b4<BKC>(buf + 3 * HALF, wc, lane, b1f);
+        read_b4<BKC>(V4_SLOT(4 * t + 2), wc, lane, b1f);
       } else if (r == 2) {
-        read_a4<AKC, BKC>(buf + HALF, wr, lane, af);
+        read_a4<AKC, BKC>(V4_SLOT(4 * t + 3), wr, lane, af);
       }
 #ifndef VIT_V4_NODMA
-      if (f + 6 < nstage) V4_STAGE(f + 6);
-      wait_stage_retired(min(4, nstage - 1 - (f + 2)));
+      if (f + V4_LEAD < nstage) V4_STAGE(f + V4_LEAD);
+      wait_stage_retired(min(V4_LEAD - 2, nstage - 1 - (f + 2)));
 #endif
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -720,6 +747,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     }
   }
 #undef V4_STAGE
+#undef V4_SLOT
   if (wr == 0) __builtin_amdgcn_s_barrier();              // balance group 1's extra barrier
 
 #if defined(VIT_V4_DIRECT_EPI)
@@ -1027,6 +1055,12 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     const bool v4 = (impl == 4 || impl == 3) && dma_ok;
     GemmArgs g4 = g;
     g4.tiles_n = (d->n + 255) / 256;
+    g4.tiles_m = (d->m + 255) / 256;
+    {
+      const char* gv = getenv("VIT_GEMM_GROUP");
+      g4.group_m = gv ? atoi(gv) : 1;
+      if (g4.group_m < 1) g4.group_m = 1;
+    }
     g4.kt_per_split = (nkt + split - 1) / split;
     dim3 grid4((unsigned)(((d->m + 255) / 256) * g4.tiles_n), (unsigned)split);
     // v4 epilogue kind
