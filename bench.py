@@ -39,6 +39,43 @@ def gflop_per_image(D, L, T, N, P, C, nc):
     return (2 * pe + 3 * (L * block + head)) / 1e9
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes (profiles/, FETCH_SIZE with
+    the gfx950 x2 correction + WRITE_SIZE; tools/r2d.sh), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r2_qkv_fwd_pmc.json")) as f:
+            return int(json.load(f)["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def gemm_peak(dev, n=8192, reps=5):
+    """Measured dense bf16 MFMA GEMM rate on this device: this library's GEMM and hipBLASLt
+    (torch.matmul) on one n^3 GEMM of uniform [-1, 1) operands, outside the timed steps."""
+    from VisionTransformer import _ops
+    g = torch.Generator(device=dev).manual_seed(7)
+    a = (torch.rand(n, n, device=dev, generator=g) * 2 - 1).bfloat16()
+    b = (torch.rand(n, n, device=dev, generator=g) * 2 - 1).bfloat16()
+    c = torch.empty(n, n, dtype=torch.bfloat16, device=dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / reps
+
+    flop = 2.0 * n ** 3
+    t_ours = timed(lambda: _ops.gemm(a, b, c, n, n, n, n, n, n))
+    t_lib = timed(lambda: torch.matmul(a, b.t(), out=c))
+    return {"shape": f"{n}x{n}x{n} bf16, uniform [-1,1)", "vit_gemm_tflops": round(flop / t_ours / 1e12, 1),
+            "hipblaslt_tflops": round(flop / t_lib / 1e12, 1)}
+
+
 def cpu_baseline(model_name, img, nc, batch=8, warmup=1, steps=3):
     from oracle import vit_oracle as O
     threads = min(16, len(os.sched_getaffinity(0)))
@@ -70,6 +107,7 @@ def main():
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,7 +207,9 @@ def main():
                          "peak": peak / 1e12, "unit": "TFLOP/s",
                          "frac": round(qkv_flop / kavg / peak, 4) if kavg > 0 else None,
                          "flop_per_launch": qkv_flop, "avg_launch_us": round(kavg * 1e6, 2),
-                         "launches_timed": len(kdur), "traffic": None},
+                         "launches_timed": len(kdur), "traffic": pmc_traffic(),
+                         "traffic_source": "profiles/r2_qkv_fwd_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"},
+            "measured_gemm_peak": None if args.no_gemm_peak else gemm_peak(dev),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.model, args.img, args.classes)

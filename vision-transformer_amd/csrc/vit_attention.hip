@@ -592,6 +592,7 @@ VIT_DEV void store_rows64(const bf16_t* img, int rows, int valid_rows, bf16_t* d
   }
 }
 
+template <int NQB>
 __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                          const bf16_t* __restrict__ d_o, const float* __restrict__ lse,
                                                          bf16_t* __restrict__ dqkv, int64_t Tn64, int64_t H,
@@ -613,8 +614,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   const int Tn = (int)Tn64;
   const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
   const int64_t D = H * HD, ld = 3 * D;
-  const int Tp = (Tn + 31) & ~31;
-  const int nqb = Tp / 32;
+  constexpr int Tp = NQB * 32;                        // T rounded up to 32 (compile time: the dQ sum unrolls)
+  constexpr int nqb = NQB;
   const float c2 = scale * LOG2E;
 
   // ---- stage K, Q, dO, O (O into the dS region: only needed for delta); lse
@@ -751,6 +752,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 
   // software pipeline: iteration i computes pair(i) (if any) and dQ(i-1) between the same two barriers
   bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
+#pragma unroll 1
   for (int it = 0; it <= nqb; ++it) {
     if (it >= 2) {                                    // dQ(it-2) staged in the previous iteration: full-row stores
       const int qs = (it - 2) * 32;
@@ -761,6 +763,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       const int qb = it - 1;
       const bf16_t* dS = dSt + (qb & 1) * DST;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
       for (int kc = 0; kc < Tp; kc += 32) {
         const bf16x8_t a = trd(Ks + kc * HD, cf_k[0], cf_k[1]);
         const bf16x8_t bq = trd(dS + kc * 32, cf_s[0], cf_s[1]);
@@ -944,8 +947,20 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, con
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_BWD_SPLIT")) {
-    attn_bwd_fused<<<(unsigned)(B * H), 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse,
-                                                     (bf16_t*)dqkv, T, H, scale);
+#define BWD(NQ)                                                                                                 \
+  attn_bwd_fused<NQ><<<(unsigned)(B * H), 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \
+                                                       (bf16_t*)dqkv, T, H, scale)
+    switch ((int)((T + 31) / 32)) {
+      case 1: BWD(1); break;
+      case 2: BWD(2); break;
+      case 3: BWD(3); break;
+      case 4: BWD(4); break;
+      case 5: BWD(5); break;
+      case 6: BWD(6); break;
+      case 7: BWD(7); break;
+      default: BWD(8); break;
+    }
+#undef BWD
   } else if (use_mfma(dtype, hd)) {
     float* delta = (float*)workspace;
     const int64_t rows = B * T * H;
