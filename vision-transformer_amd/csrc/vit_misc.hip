@@ -120,16 +120,22 @@ __global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2(const float* __r
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   part += (int64_t)blockIdx.y * nchunks * cols;
   float* __restrict__ out = blockIdx.y == 0 ? outs.p[0] : (blockIdx.y == 1 ? outs.p[1] : outs.p[2]);
-  float s0 = 0.f, s1 = 0.f;
+  // 8 independent chains per lane (chunk k goes to chain (k / CS2_WAVES) % 8): 8 loads in flight per lane, order fixed
+  constexpr int CH = 8;
+  float sc[CH];
+#pragma unroll
+  for (int i = 0; i < CH; ++i) sc[i] = 0.f;
   if (c < cols) {
     int64_t k = w;
-    for (; k + CS2_WAVES < nchunks; k += 2 * CS2_WAVES) {   // two independent chains per lane
-      s0 += part[k * cols + c];
-      s1 += part[(k + CS2_WAVES) * cols + c];
+    for (; k + (CH - 1) * CS2_WAVES < nchunks; k += CH * CS2_WAVES) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) sc[i] += part[(k + i * CS2_WAVES) * cols + c];
     }
-    if (k < nchunks) s0 += part[k * cols + c];
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      if (k + i * CS2_WAVES < nchunks) sc[i] += part[(k + i * CS2_WAVES) * cols + c];
   }
-  red[w][lane] = s0 + s1;
+  red[w][lane] = ((sc[0] + sc[1]) + (sc[2] + sc[3])) + ((sc[4] + sc[5]) + (sc[6] + sc[7]));
   __syncthreads();
   if (w == 0 && c < cols) {
     float s = 0.f;
