@@ -647,6 +647,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     if (c == 0) dlts[r] = sacc;
   }
   __syncthreads();                                    // delta visible; the O image (dS region) is dead
+#ifdef VIT_AB_ONLYSTAGE
+  if (dlts[tid & 127] == 1234.5f) dqkv[tid] = 0;   // keep the staging live; no compute
+  return;
+#endif
 
   const bool kact = wave < nqb;                       // this wave owns key block `wave`
   const int kb = wave * 32;
@@ -758,7 +762,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       const int qs = (it - 2) * 32;
       store_rows64(dQs + ((it - 2) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
     }
+#ifndef VIT_AB_NOPAIR
     if (kact && it < nqb) pair(it);
+#endif
+#ifndef VIT_AB_NODQ
     if (it >= 1) {
       const int qb = it - 1;
       const bf16_t* dS = dSt + (qb & 1) * DST;
@@ -773,6 +780,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
       st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * 64 + dd * 16 + 4 * (lane >> 4), v4);
     }
+#endif
     __syncthreads();
   }
   {                                                   // last dQ block
