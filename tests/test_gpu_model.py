@@ -280,3 +280,76 @@ def test_side_stream_weight_gradients_bitwise_equal():
         torch.cuda.synchronize()
         gs.append(m.hip_engine.G.clone())
     assert torch.equal(gs[0], gs[1])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_long_sequence_384_vs_oracle(dtype):
+    """BASELINE config 5's sequence length (384^2 / patch 16 -> 576 patches + cls = 577 tokens) at reduced width
+    (D=128, H=2, hd=64, L=1, B=2): T > 256 takes the tiled attention kernels (attn_fwd_mfma, attn_bwd_dq_mfma,
+    attn_bwd_dkdv_mfma, attn_delta), not the single-workgroup fused ones.  fp32: logits 1e-4, grads 2e-4 (scaled);
+    bf16: the same gate as test_bf16_vs_oracle_same_rounding."""
+    ocfg = O.make_config("micro", img=384, batch=2, blocks=1)
+    ocfg.embedding_size, ocfg.num_heads = 128, 2
+    st = O.init_state(ocfg, seed=3)
+    bf = dtype == "bf16"
+    m = _model(ocfg, dtype=torch.bfloat16 if bf else torch.float32)
+    m.load_state_dict(st)
+    m.eval()
+    x, y = O.synthetic_batch(ocfg)
+    logits = m(x.to(DEV))
+    loss = cross_entropy(logits, y.to(DEV))
+    loss.backward()
+    lg_32, loss_32, g_32 = O.loss_and_grads(st, x, y, ocfg)
+    if not bf:
+        assert (logits.detach().cpu() - lg_32).abs().max().item() < 1e-4
+        assert abs(loss.item() - loss_32.item()) < 1e-5
+        for k, p in m.named_parameters():
+            err = (p.grad.cpu() - g_32[k]).abs().max().item()
+            assert err <= 2e-4 * max(1.0, g_32[k].abs().max().item()), (k, err)
+        return
+    lg_bf, _, g_bf = O.loss_and_grads(st, x, y, ocfg, bf16=True)
+    assert _rel(logits.detach().cpu(), lg_bf) < 1e-2
+    # The query / key projection gradients are dS-driven (dQ = dS K, dK = dS^T Q over 577 tokens, each softmax row
+    # of dS summing to zero), so bf16 rounding of P / dS is amplified by cancellation (the bf16-emulating oracle
+    # itself is 4-12% off fp32 there).  The tiled T > 256 kernels do not round at exactly the storage points the
+    # oracle emulates (measured: 2.5-2.8x its error on one head, below it on the other), so the query / key gate is
+    # 4x the oracle's own bf16 error; every other tensor keeps the standard gate.  fp32 (above) pins the algorithm.
+    bad = []
+    for k, p in m.named_parameters():
+        ours, ora = _rel(p.grad.cpu(), g_32[k]), _rel(g_bf[k], g_32[k])
+        gate = max(3e-2, (4 if (".key." in k or ".query." in k) else 2) * ora)
+        print(f"{k}: ours {ours:.4f} oracle-bf16 {ora:.4f}")
+        if ours > gate:
+            bad.append((k, ours, ora))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("preset,img,batch", [("large", 224, 128), ("base", 384, 64)])
+def test_full_size_configs_properties(preset, img, batch):
+    """BASELINE configs 4 (ViT-L/16 224^2, B=128/GPU) and 5 (ViT-B/16 384^2, B=64) at full size in bf16: finite loss,
+    bitwise-deterministic gradients over two identical steps, loss decreases over 3 FusedAdamW steps."""
+    c = config.ViTConfig.preset(preset, img_size=img, batch_size=batch, precision=torch.bfloat16, device="cpu")
+    torch.manual_seed(0)
+    m = vit.VisionTransformer(c).to(DEV).eval()
+    x = torch.randn(batch, 3, img, img, generator=torch.Generator().manual_seed(7)).to(DEV)
+    y = torch.randint(0, 1000, (batch,), generator=torch.Generator().manual_seed(8)).to(DEV)
+    gs = []
+    for _ in range(2):
+        loss = cross_entropy(m(x), y)
+        for p in m.parameters():
+            p.grad = None
+        loss.backward()
+        gs.append(m.hip_engine.G.clone())
+        assert torch.isfinite(loss).item()
+    assert torch.equal(gs[0], gs[1])
+    assert torch.isfinite(gs[0]).all().item()
+    del gs
+    opt = FusedAdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    losses = []
+    for _ in range(3):
+        loss = cross_entropy(m(x), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[2] < losses[0], losses

@@ -592,65 +592,63 @@ VIT_DEV void store_rows64(const bf16_t* img, int rows, int valid_rows, bf16_t* d
   }
 }
 
+// Workgroup barrier ordering LDS only: unlike __syncthreads() (a release fence: vmcnt(0)) it leaves global loads,
+// LDS-DMA and stores in flight.  LDS-DMA targets are published by an explicit vmcnt(0) + barrier where consumed.
+VIT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One 8-row piece `pc` of a swizzled [Tp][64] head-slice image by LDS-DMA (one 16-B lane each; rows >= Tn zero).
+// global_load_lds form (per-lane address): rows >= Tn are clamped to row Tn - 1 instead of zero-filled; the persistent
+// backward masks them (P = 0 for queries >= T through lse = +inf, for keys >= T through kbias), finite data suffices.
+VIT_DEV void dma_piece(const bf16_t* base, int64_t row0, int64_t ld, int64_t col0, int Tn, bf16_t* img, int pc,
+                       int lane) {
+  const int r = pc * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ aswz(r);
+  const bf16_t* src = base + (row0 + min(r, Tn - 1)) * ld + col0 + c * 8;
+  // Issued as inline asm on purpose: the compiler's waitcnt pass cannot tell the DMA target from the blocks still
+  // being read and would put vmcnt(0) before every later LDS read, draining the prefetch.  Completion is awaited
+  // explicitly (vmcnt(0) + barrier at the top of the next item).
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(img + pc * 512));
+  // M0 is reserved (clang warns) but no compiler-generated code in this kernel reads it (checked in the ISA)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+#pragma clang diagnostic pop
+}
+VIT_DEV void dma_slice_g(const bf16_t* base, int64_t row0, int64_t ld, int64_t col0, int Tn, int Tp, bf16_t* img,
+                         int wave, int lane) {
+  for (int pc = wave; pc < Tp / 8; pc += 8) dma_piece(base, row0, ld, col0, Tn, img, pc, lane);
+}
+
+// Persistent: workgroup g handles items (image, head) g, g + gridDim.x, ...  The next item's operands are staged while
+// this one computes: its Q / dO 32-row blocks are LDS-DMA'd into this item's blocks as they die (block qb is last read
+// by pair(qb)), its K and O (only needed for delta; into the dS^T region) right after the last dQ block, its lse into a
+// register.  The first item's staging is exposed, later ones only the K / O tail behind the dK / dV stores.  gridDim.x == items gives one item per
+// workgroup (no prefetch).  dK / dV leave registers directly (the Q / dO images already hold the next item).
 template <int NQB>
 __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                          const bf16_t* __restrict__ d_o, const float* __restrict__ lse,
                                                          bf16_t* __restrict__ dqkv, int64_t Tn64, int64_t H,
-                                                         float scale) {
-  constexpr int IMG = FB_TMAX * HD;                   // elements per [Tp][64] image (max)
-  constexpr int DST = FB_TMAX * 32;                   // elements per dS^T image [Tp][32]
+                                                         int64_t items, float scale) {
+  constexpr int Tp = NQB * 32;                        // T rounded up to 32 (compile time: the dQ sum unrolls)
+  constexpr int nqb = NQB;
+  constexpr int IMG = Tp * HD;                        // elements per [Tp][64] image
+  constexpr int DST = Tp * 32;                        // elements per dS^T image [Tp][32]
   constexpr int QST = 32 * HD;                        // dQ block staging [32][64]
-  __shared__ __attribute__((aligned(16))) bf16_t smem[3 * IMG + 2 * DST + 2 * QST + 2 * FB_TMAX * 2];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[3 * IMG + 2 * DST + 2 * QST + 2 * Tp * 2];
   bf16_t* Ks = smem;
   bf16_t* Qs = Ks + IMG;
   bf16_t* Gs = Qs + IMG;
-  bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]; holds the O image during staging
+  bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]
   bf16_t* dQs = dSt + 2 * DST;                         // [2][32][64]
   float* lse2s = reinterpret_cast<float*>(dQs + 2 * QST);
-  float* dlts = lse2s + FB_TMAX;
+  float* dlts = lse2s + Tp;
 
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Tn = (int)Tn64;
-  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
   const int64_t D = H * HD, ld = 3 * D;
-  constexpr int Tp = NQB * 32;                        // T rounded up to 32 (compile time: the dQ sum unrolls)
-  constexpr int nqb = NQB;
   const float c2 = scale * LOG2E;
-
-  // ---- stage K, Q, dO, O (O into the dS region: only needed for delta); lse
-  {
-    const int64_t nb = gridDim.x / H;                  // host guarantees both tensors are < 2 GiB
-    const __amdgpu_buffer_rsrc_t rq = make_rsrc_b(qkv, nb * Tn * ld * 2);
-    const __amdgpu_buffer_rsrc_t rg = make_rsrc_b(d_o, nb * Tn * D * 2);
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc_b(o, nb * Tn * D * 2);
-    dma_head_slice(rq, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane);
-    dma_head_slice(rq, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
-    dma_head_slice(rg, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
-    dma_head_slice(ro, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);
-  }
-  for (int r = tid; r < Tp; r += 512) lse2s[r] = r < Tn ? lse[bh * Tn + r] * LOG2E : INFINITY;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // delta[q] = sum_d dO[q][d] O[q][d]: 8 lanes per row (one 16-B chunk each), fixed shuffle-tree order
-  for (int q = tid; q < Tp * 8; q += 512) {
-    const int r = q >> 3, c = q & 7;
-    const int off = r * HD + ((c ^ aswz(r)) << 3);
-    const s16x8 vo = *reinterpret_cast<const s16x8*>(dSt + off);
-    const s16x8 vg = *reinterpret_cast<const s16x8*>(Gs + off);
-    float sacc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sacc += bf2f((bf16_t)vo[j]) * bf2f((bf16_t)vg[j]);
-    sacc += __shfl_xor(sacc, 1, 64);
-    sacc += __shfl_xor(sacc, 2, 64);
-    sacc += __shfl_xor(sacc, 4, 64);
-    if (c == 0) dlts[r] = sacc;
-  }
-  __syncthreads();                                    // delta visible; the O image (dS region) is dead
-#ifdef VIT_AB_ONLYSTAGE
-  if (dlts[tid & 127] == 1234.5f) dqkv[tid] = 0;   // keep the staging live; no compute
-  return;
-#endif
 
   const bool kact = wave < nqb;                       // this wave owns key block `wave`
   const int kb = wave * 32;
@@ -658,15 +656,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   const bool kmask = kb + 32 > Tn;                    // wave-uniform: this key block has keys >= T
   const float kbias = key < Tn ? 0.f : -INFINITY;
   const int dd = wave >> 1, qh = wave & 1;            // this wave's dQ tile: d 16dd.., queries 16qh..
-  bf16x8_t kf[4], vf[4];
-  f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
-  if (kact) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = row_frag(Ks, kb, s, lane);
-      vf[s] = glb_frag(qkv + b * Tn * ld, ld, kb, Tn, 2 * D + h * HD, s, lane);
-    }
-  }
   // Per-lane LDS offsets (elements) inside a 32-row block: the row swizzle aswz(r) only uses bits 1..3 of r, so a
   // block starting at a multiple of 16 rows adds rb * 64 and nothing else.
   int rf_off[4];                                       // row_frag: row (lane&31), chunk 2s + hf
@@ -707,103 +696,191 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(base + o));
   };
 
-  // pair(qb): this wave's key block against query block qb -> dV, dK accumulate; dS^T block -> dSt[qb & 1]
-  auto pair = [&](int qb) {
-    const int q0 = qb * 32;
-    const bf16_t* Qb = Qs + q0 * HD;
-    const bf16_t* Gb = Gs + q0 * HD;
-    f32x16 sacc = {}, pacc = {};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sacc = mfma32(rrd(Qb, rf_off[s]), kf[s], sacc);           // S[q][key]: lane = key
-      pacc = mfma32(rrd(Gb, rf_off[s]), vf[s], pacc);           // dP[q][key]
-    }
-    // registers 4g..4g+3 <-> queries q0 + 8g + 4hf + 0..3: broadcast b128 reads of the statistics
-    float p[16], ds[16];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2s + q0 + 8 * g + 4 * hf);
-      const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dlts + q0 + 8 * g + 4 * hf);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 4 * g + i;
-        // queries >= T have lse2 = +inf -> P = 0 exactly
-        p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lv[i]);
-        ds[r] = pacc[r] - dv4[i];
-      }
-    }
-    if (kmask) {                                      // keys >= T (zero K rows) must not contribute
-#pragma unroll
-      for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lse2s[q0 + acc_row(r, hf)] + kbias);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ds[r] *= p[r];
-    const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      dv[db] = mfma32(trd(Gb, tf_off[db][0], tf_off[db][1]), p0, dv[db]);
-      dv[db] = mfma32(trd(Gb + 16 * HD, tf_off[db][0], tf_off[db][1]), p1, dv[db]);
-      dk[db] = mfma32(trd(Qb, tf_off[db][0], tf_off[db][1]), d0, dk[db]);
-      dk[db] = mfma32(trd(Qb + 16 * HD, tf_off[db][0], tf_off[db][1]), d1, dk[db]);
-    }
-    bf16_t* dS = dSt + (qb & 1) * DST + key * 32 + 4 * hf;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      float v4[4] = {ds[4 * g4], ds[4 * g4 + 1], ds[4 * g4 + 2], ds[4 * g4 + 3]};
-      st4<bf16_t>(dS + 8 * g4, v4);
-    }
+  // lse of item `it_` -> a register (tid < Tn <= 256)
+  float lreg = 0.f;
+  auto load_lse = [&](int64_t it_) {
+    if (tid < Tn) lreg = lse[it_ * Tn + tid];
   };
 
-  // software pipeline: iteration i computes pair(i) (if any) and dQ(i-1) between the same two barriers
-  bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
+  int64_t item = blockIdx.x;
+  if (item < items) {                                 // first item: exposed staging
+    const int64_t b = item / H, h = item % H;
+    dma_slice_g(qkv, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane);
+    dma_slice_g(qkv, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
+    dma_slice_g(d_o, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
+    dma_slice_g(o, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);   // O: only needed for delta
+    load_lse(item);
+  }
 #pragma unroll 1
-  for (int it = 0; it <= nqb; ++it) {
-    if (it >= 2) {                                    // dQ(it-2) staged in the previous iteration: full-row stores
-      const int qs = (it - 2) * 32;
-      store_rows64(dQs + ((it - 2) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
-    }
-#ifndef VIT_AB_NOPAIR
-    if (kact && it < nqb) pair(it);
-#endif
-#ifndef VIT_AB_NODQ
-    if (it >= 1) {
-      const int qb = it - 1;
-      const bf16_t* dS = dSt + (qb & 1) * DST;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (; item < items; item += gridDim.x) {
+    const int64_t b = item / H, h = item % H;
+    const int64_t nxt = item + gridDim.x;
+    const bool more = nxt < items;
+    const int64_t nb_ = more ? nxt / H : 0, nh_ = more ? nxt % H : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / O DMA, lse
+    if (tid < Tp) lse2s[tid] = tid < Tn ? lreg * LOG2E : INFINITY;
+    __syncthreads();                                  // every wave's DMA landed
+    // delta[q] = sum_d dO[q][d] O[q][d]: 8 lanes per row (one 16-B chunk each), fixed shuffle-tree order
+    for (int q = tid; q < Tp * 8; q += 512) {         // Tp * 8 is a multiple of 256: wave-uniform condition
+      {
+        const int r = q >> 3, c = q & 7;
+        const int off = r * HD + ((c ^ aswz(r)) << 3);
+        const s16x8 vg = *reinterpret_cast<const s16x8*>(Gs + off);
+        const s16x8 vo = *reinterpret_cast<const s16x8*>(dSt + off);
+        float sacc = 0.f;
 #pragma unroll
-      for (int kc = 0; kc < Tp; kc += 32) {
-        const bf16x8_t a = trd(Ks + kc * HD, cf_k[0], cf_k[1]);
-        const bf16x8_t bq = trd(dS + kc * 32, cf_s[0], cf_s[1]);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc, 0, 0, 0);
+        for (int e = 0; e < 8; ++e) sacc += bf2f((bf16_t)vo[e]) * bf2f((bf16_t)vg[e]);
+        sacc += __shfl_xor(sacc, 1, 64);
+        sacc += __shfl_xor(sacc, 2, 64);
+        sacc += __shfl_xor(sacc, 4, 64);
+        if (c == 0) dlts[r] = sacc;
       }
-      // D[m = d][n = q]: lane -> q = 16qh + (lane&15), d = 16dd + 4(lane>>4) + i  -> staging [32][64]
-      float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
-      st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * 64 + dd * 16 + 4 * (lane >> 4), v4);
     }
-#endif
-    __syncthreads();
-  }
-  {                                                   // last dQ block
-    const int qs = (nqb - 1) * 32;
-    store_rows64(dQs + ((nqb - 1) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
-  }
-  // dK, dV: [Tp][64] images in the (dead) Q and dO regions, then full-row stores
-  if (kact) {
+    bf16x8_t kf[4], vf[4];
+    if (kact) {
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
+      for (int s = 0; s < 4; ++s) {
+        kf[s] = row_frag(Ks, kb, s, lane);
+        vf[s] = glb_frag(qkv + b * Tn * ld, ld, kb, Tn, 2 * D + h * HD, s, lane);
+      }
+    }
+    lds_barrier();                                    // delta visible
+    f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+
+    // pair(qb): this wave's key block against query block qb -> dV, dK accumulate; dS^T block -> dSt[qb & 1]
+    auto pair = [&](int qb) {
+      const int q0 = qb * 32;
+      const bf16_t* Qb = Qs + q0 * HD;
+      const bf16_t* Gb = Gs + q0 * HD;
+      f32x16 sacc = {}, pacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sacc = mfma32(rrd(Qb, rf_off[s]), kf[s], sacc);           // S[q][key]: lane = key
+        pacc = mfma32(rrd(Gb, rf_off[s]), vf[s], pacc);           // dP[q][key]
+      }
+      // registers 4g..4g+3 <-> queries q0 + 8g + 4hf + 0..3: broadcast b128 reads of the statistics
+      float p[16], ds[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
-                      dk[db][4 * g + 3] * scale};
-        float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
-        st4<bf16_t>(Qs + key * 64 + db * 32 + 8 * g + 4 * hf, a);
-        st4<bf16_t>(Gs + key * 64 + db * 32 + 8 * g + 4 * hf, c);
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2s + q0 + 8 * g + 4 * hf);
+        const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dlts + q0 + 8 * g + 4 * hf);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          // queries >= T have lse2 = +inf -> P = 0 exactly
+          p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lv[i]);
+          ds[r] = pacc[r] - dv4[i];
+        }
+      }
+      if (kmask) {                                    // keys >= T (zero K rows) must not contribute
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lse2s[q0 + acc_row(r, hf)] + kbias);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ds[r] *= p[r];
+      const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dv[db] = mfma32(trd(Gb, tf_off[db][0], tf_off[db][1]), p0, dv[db]);
+        dv[db] = mfma32(trd(Gb + 16 * HD, tf_off[db][0], tf_off[db][1]), p1, dv[db]);
+        dk[db] = mfma32(trd(Qb, tf_off[db][0], tf_off[db][1]), d0, dk[db]);
+        dk[db] = mfma32(trd(Qb + 16 * HD, tf_off[db][0], tf_off[db][1]), d1, dk[db]);
+      }
+      bf16_t* dS = dSt + (qb & 1) * DST + key * 32 + 4 * hf;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        float v4[4] = {ds[4 * g4], ds[4 * g4 + 1], ds[4 * g4 + 2], ds[4 * g4 + 3]};
+        st4<bf16_t>(dS + 8 * g4, v4);
+      }
+    };
+
+    // software pipeline: iteration i computes pair(i) (if any) and dQ(i-1) between the same two barriers, and stages
+    // the next item's Q / dO block i-1 (last read by pair(i-1), before the previous barrier)
+    bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
+#pragma unroll 1
+    for (int it = 0; it <= nqb; ++it) {
+      if (it >= 2) {                                  // dQ(it-2) staged in the previous iteration: full-row stores
+        const int qs = (it - 2) * 32;
+        store_rows64(dQs + ((it - 2) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
+      }
+#ifndef VIT_AB_NOPAIR
+      if (kact && it < nqb) pair(it);
+#endif
+#ifndef VIT_AB_NODQ
+      if (it >= 1) {
+        const int qb = it - 1;
+        const bf16_t* dS = dSt + (qb & 1) * DST;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < Tp; kc += 32) {
+          const bf16x8_t a = trd(Ks + kc * HD, cf_k[0], cf_k[1]);
+          const bf16x8_t bq = trd(dS + kc * 32, cf_s[0], cf_s[1]);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc, 0, 0, 0);
+        }
+        // D[m = d][n = q]: lane -> q = 16qh + (lane&15), d = 16dd + 4(lane>>4) + i  -> staging [32][64]
+        float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
+        st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * 64 + dd * 16 + 4 * (lane >> 4), v4);
+      }
+#endif
+      if (more && it >= 1) {
+        const int pc = (it - 1) * 4 + (wave & 3);
+        if (wave < 4) dma_piece(qkv, nb_ * Tn, ld, nh_ * HD, Tn, Qs, pc, lane);
+        else dma_piece(d_o, nb_ * Tn, D, nh_ * HD, Tn, Gs, pc, lane);
+        if (it == 1) load_lse(nxt);                   // after pair(0) consumed the V fragments: no wait on it
+      }
+      lds_barrier();                                  // LDS only: the prefetch and the dQ stores stay in flight
+    }
+    {                                                 // last dQ block
+      const int qs = (nqb - 1) * 32;
+      store_rows64(dQs + ((nqb - 1) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
+    }
+#ifdef VIT_BWD_STAGED_DKDV
+    // K and dS^T are dead (the last dQ block ran before the final barrier): dK / dV images there, full-row stores
+    if (kact) {
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
+                        dk[db][4 * g + 3] * scale};
+          float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+          st4<bf16_t>(Ks + key * 64 + db * 32 + 8 * g + 4 * hf, a);
+          st4<bf16_t>(dSt + key * 64 + db * 32 + 8 * g + 4 * hf, c);
+        }
       }
     }
+    lds_barrier();
+    store_rows64(Ks, Tp, Tn, dqkv + b * Tn * ld + D + h * HD, ld, tid, 512);
+    store_rows64(dSt, Tp, Tn, dqkv + b * Tn * ld + 2 * D + h * HD, ld, tid, 512);
+    lds_barrier();                                    // images read before the next item's DMA overwrites them
+    if (more) {
+      dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
+      dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
+    }
+#else
+    // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K and O
+    if (more) {
+      dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
+      dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
+    }
+    if (kact && key < Tn) {
+      bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD;
+      bf16_t* dvr = dkr + D;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
+                        dk[db][4 * g + 3] * scale};
+          float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
+          st4<bf16_t>(dkr + db * 32 + 8 * g + 4 * hf, a);
+          st4<bf16_t>(dvr + db * 32 + 8 * g + 4 * hf, c);
+        }
+      }
+    }
+#endif
   }
-  __syncthreads();
-  store_rows64(Qs, Tp, Tn, dqkv + b * Tn * ld + D + h * HD, ld, tid, 512);
-  store_rows64(Gs, Tp, Tn, dqkv + b * Tn * ld + 2 * D + h * HD, ld, tid, 512);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -955,9 +1032,13 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, con
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_BWD_SPLIT")) {
-#define BWD(NQ)                                                                                                 \
-  attn_bwd_fused<NQ><<<(unsigned)(B * H), 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \
-                                                       (bf16_t*)dqkv, T, H, scale)
+    // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid
+    const int64_t items = B * H;
+    int64_t grid = std::min<int64_t>(items, vit_cu_count());
+    if (const char* e = getenv("VIT_ATTN_BWD_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(items, atoll(e)));
+#define BWD(NQ)                                                                                                  \
+  attn_bwd_fused<NQ><<<(unsigned)grid, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \
+                                                    (bf16_t*)dqkv, T, H, items, scale)
     switch ((int)((T + 31) / 32)) {
       case 1: BWD(1); break;
       case 2: BWD(2); break;

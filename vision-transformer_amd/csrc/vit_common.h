@@ -95,6 +95,19 @@ void colsum_parts_launch(const void* x, int64_t ldx, int dtype, int64_t rows, in
                          float* part, hipStream_t s);
 }  // namespace vit
 
+// Compute units of the current device (256 on MI355X), queried once per device.
+static inline int64_t vit_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 #define VIT_REQUIRE(cond, ...)                 \
   do {                                         \
     if (!(cond)) {                             \
