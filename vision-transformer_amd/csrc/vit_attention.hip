@@ -635,13 +635,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   constexpr int IMG = Tp * HD;                        // elements per [Tp][64] image
   constexpr int DST = Tp * 32;                        // elements per dS^T image [Tp][32]
   constexpr int QST = 32 * HD;                        // dQ block staging [32][64]
-  __shared__ __attribute__((aligned(16))) bf16_t smem[3 * IMG + 2 * DST + 2 * QST + 2 * Tp * 2];
+  // V image too when it fits in the 160 KiB (Tp <= 224): staged during the previous item instead of read from global
+  // at the top of each item (an exposed load round trip per item)
+  constexpr bool VLDS = (4 * IMG + 2 * DST + 2 * QST + 2 * Tp * 2) * 2 <= 160 * 1024;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(VLDS ? 4 : 3) * IMG + 2 * DST + 2 * QST + 2 * Tp * 2];
   bf16_t* Ks = smem;
   bf16_t* Qs = Ks + IMG;
   bf16_t* Gs = Qs + IMG;
   bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]
   bf16_t* dQs = dSt + 2 * DST;                         // [2][32][64]
-  float* lse2s = reinterpret_cast<float*>(dQs + 2 * QST);
+  bf16_t* Vs = dQs + 2 * QST;                          // [Tp][64] when VLDS
+  float* lse2s = reinterpret_cast<float*>(Vs + (VLDS ? IMG : 0));
   float* dlts = lse2s + Tp;
 
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
@@ -709,6 +713,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     dma_slice_g(qkv, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
     dma_slice_g(d_o, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
     dma_slice_g(o, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);   // O: only needed for delta
+    if (VLDS) dma_slice_g(qkv, b * Tn, ld, 2 * D + h * HD, Tn, Tp, Vs, wave, lane);
     load_lse(item);
   }
 #pragma unroll 1
@@ -741,7 +746,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         kf[s] = row_frag(Ks, kb, s, lane);
-        vf[s] = glb_frag(qkv + b * Tn * ld, ld, kb, Tn, 2 * D + h * HD, s, lane);
+        vf[s] = VLDS ? row_frag(Vs, kb, s, lane) : glb_frag(qkv + b * Tn * ld, ld, kb, Tn, 2 * D + h * HD, s, lane);
       }
     }
     lds_barrier();                                    // delta visible
@@ -827,7 +832,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         const int pc = (it - 1) * 4 + (wave & 3);
         if (wave < 4) dma_piece(qkv, nb_ * Tn, ld, nh_ * HD, Tn, Qs, pc, lane);
         else dma_piece(d_o, nb_ * Tn, D, nh_ * HD, Tn, Gs, pc, lane);
-        if (it == 1) load_lse(nxt);                   // after pair(0) consumed the V fragments: no wait on it
+        if (it == 1) {
+          load_lse(nxt);                              // after pair(0) consumed the V fragments: no wait on it
+          if (VLDS) dma_slice_g(qkv, nb_ * Tn, ld, 2 * D + nh_ * HD, Tn, Tp, Vs, wave, lane);  // V read at the top
+        }
       }
       lds_barrier();                                  // LDS only: the prefetch and the dQ stores stay in flight
     }
