@@ -283,11 +283,11 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16_t* __restrict__ 
       }
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       const float m_new = fmaxf(m_run, mloc);
-      const float alpha = exp2f(m_run - m_new);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float psum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        x[r] = exp2f(x[r] - m_new);
+        x[r] = __builtin_amdgcn_exp2f(x[r] - m_new);
         psum += x[r];
       }
       l_run = l_run * alpha + psum;
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t key = key0 + acc_row(r, hf);
-        const float p = key < Tn ? exp2f(sacc[r] * c2 - lse2) : 0.f;
+        const float p = key < Tn ? __builtin_amdgcn_exp2f(sacc[r] * c2 - lse2) : 0.f;
         ds[r] = p * (pacc[r] - dl);
       }
       const bf16x8_t d0 = pack8(ds), d1 = pack8(ds + 8);
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restri
         const int qr = qb + acc_row(r, hf);
         const float l2 = stat[cur][0][qr], dlt = stat[cur][1][qr];
         const bool valid = qrow0 + acc_row(r, hf) < Tn;
-        p[r] = valid ? exp2f(sacc[r] * c2 - l2) : 0.f;
+        p[r] = valid ? __builtin_amdgcn_exp2f(sacc[r] * c2 - l2) : 0.f;
         ds[r] = p[r] * (pacc[r] - dlt);
       }
       const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
@@ -944,11 +944,11 @@ __global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restr
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float m_new = fmaxf(m_run, mloc);
-    const float alpha = exp2f(m_run - m_new);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     float psum = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      x[r] = exp2f(x[r] - m_new);
+      x[r] = __builtin_amdgcn_exp2f(x[r] - m_new);
       psum += x[r];
     }
     l_run = l_run * alpha + psum;
