@@ -27,8 +27,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--T", type=int, default=197, help="tokens (577 = 384^2 / patch 16 + cls: the tiled kernels)")
     args = ap.parse_args()
-    B, T, H, hd = args.batch, 197, 12, 64
+    B, T, H, hd = args.batch, args.T, 12, 64
     D = H * hd
     torch.manual_seed(0)
     qkv = (torch.randn(B * T, 3 * D, device="cuda") * 0.5).bfloat16()

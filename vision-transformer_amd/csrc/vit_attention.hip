@@ -364,8 +364,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
     qf[s] = glb_frag(base, ld, q0, Tn, h * HD, s, lane);
     gf[s] = glb_frag(d_o + b * Tn * D, D, q0, Tn, h * HD, s, lane);
   }
-  const float lse2 = q < Tn ? lse[bh * Tn + q] * LOG2E : 0.f;
-  const float dl = q < Tn ? delta[bh * Tn + q] : 0.f;
+  const float nls = q < Tn ? -lse[bh * Tn + q] / scale : 0.f;   // initial S accumulator (row constant)
+  const float ndl = q < Tn ? -delta[bh * Tn + q] : 0.f;          // initial dP accumulator
   f32x16 dq[2] = {f32x16{}, f32x16{}};
   const int ntiles = (int)((Tn + KT - 1) / KT);
   uint4 rk[2], rv[2];
@@ -386,19 +386,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = sub * 32;
-      f32x16 sacc = {}, pacc = {};
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = nls;
+        pacc[r] = ndl;
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        sacc = mfma32(row_frag(Ks, kb, s, lane), qf[s], sacc);
-        pacc = mfma32(row_frag(Vs, kb, s, lane), gf[s], pacc);
+        sacc = mfma32(row_frag(Ks, kb, s, lane), qf[s], sacc);  // S' = S - lse / scale
+        pacc = mfma32(row_frag(Vs, kb, s, lane), gf[s], pacc);  // dP' = dP - delta
       }
       const int64_t key0 = (int64_t)t * KT + kb;
       float ds[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t key = key0 + acc_row(r, hf);
-        const float p = key < Tn ? __builtin_amdgcn_exp2f(sacc[r] * c2 - lse2) : 0.f;
-        ds[r] = p * (pacc[r] - dl);
+      for (int r = 0; r < 16; ++r) ds[r] = __builtin_amdgcn_exp2f(sacc[r] * c2) * pacc[r];
+      if (key0 + 32 > Tn) {                           // wave-uniform: keys >= T (zero K rows) must not contribute
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key0 + acc_row(r, hf) >= Tn) ds[r] = 0.f;
       }
       const bf16x8_t d0 = pack8(ds), d1 = pack8(ds + 8);
 #pragma unroll
@@ -434,7 +440,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restri
                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                           int64_t Tn, int64_t H, float scale) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];  // [buf][Q, dO]
-  __shared__ float stat[2][2][KT];                                     // [buf][lse2, delta]
+  // [buf][-lse / scale, -delta] per query: the initial S / dP accumulators (rows >= T: -inf -> P = 0)
+  __shared__ __attribute__((aligned(16))) float stat[2][2][KT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
   const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
   const int64_t D = H * HD, ld = 3 * D;
@@ -455,8 +462,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restri
   auto load_stats = [&](int t) {
     if (tid < KT) {
       const int64_t qq = (int64_t)t * KT + tid;
-      st_l = qq < Tn ? lse[bh * Tn + qq] * LOG2E : 0.f;
-      st_d = qq < Tn ? delta[bh * Tn + qq] : 0.f;
+      st_l = qq < Tn ? -lse[bh * Tn + qq] / scale : -INFINITY;
+      st_d = qq < Tn ? -delta[bh * Tn + qq] : 0.f;
     }
   };
   tile_load(base, ld, 0, Tn, h * HD, tid, rq);
@@ -482,21 +489,29 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restri
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int qb = sub * 32;
-      f32x16 sacc = {}, pacc = {};
+      // row constants as the initial accumulators: S' = S - lse / scale, dP' = dP - delta (registers 4g..4g+3 <->
+      // queries qb + 8g + 4hf + 0..3: b128 broadcast reads)
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(&stat[cur][0][qb + 8 * g + 4 * hf]);
+        const f32x4 dv4 = *reinterpret_cast<const f32x4*>(&stat[cur][1][qb + 8 * g + 4 * hf]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sacc[4 * g + i] = lv[i];
+          pacc[4 * g + i] = dv4[i];
+        }
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        sacc = mfma32(row_frag(Qs, qb, s, lane), kf[s], sacc);   // S[q][key]
-        pacc = mfma32(row_frag(Gs, qb, s, lane), vf[s], pacc);   // dP[q][key]
+        sacc = mfma32(row_frag(Qs, qb, s, lane), kf[s], sacc);   // S'[q][key]
+        pacc = mfma32(row_frag(Gs, qb, s, lane), vf[s], pacc);   // dP'[q][key]
       }
-      const int64_t qrow0 = (int64_t)t * KT + qb;
       float p[16], ds[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int qr = qb + acc_row(r, hf);
-        const float l2 = stat[cur][0][qr], dlt = stat[cur][1][qr];
-        const bool valid = qrow0 + acc_row(r, hf) < Tn;
-        p[r] = valid ? __builtin_amdgcn_exp2f(sacc[r] * c2 - l2) : 0.f;
-        ds[r] = p[r] * (pacc[r] - dlt);
+        p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2);           // queries >= T: -inf -> 0
+        ds[r] = p[r] * pacc[r];
       }
       const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
 #pragma unroll
