@@ -436,7 +436,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv,
                                                           const bf16_t* __restrict__ d_o,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
