@@ -234,7 +234,7 @@ VIT_DEV f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 // row index (within a 32-row MFMA tile) of accumulator register r for lane half h
 VIT_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-__global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+__global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                      float* __restrict__ lse, int64_t Tn, int64_t H, float scale) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];  // [buf][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
