@@ -8,15 +8,23 @@ FusedAdamW step.  Weak scaling: every rank processes its own batch of 256.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
-Rank 0 prints ONE JSON line.  `roofline` is measured live: HIP events on the compute stream bracket every launch of
-the dominant kernel family's representative GEMM (the fused QKV projection forward, M=B*T, N=3D, K=D: one launch of
-gemm_bf16_v4<kcontig, kcontig, bf16, EPI_PLAIN>) inside the timed steps.
-`cpu_baseline` times the oracle port (oracle/vit_oracle.py: the reference's algorithm restated in torch on CPU) on
-the host cores, rank 0 at N=1 only, on a bounded sample (ViT-B/16 224^2 fp32, batch 8, 1 warmup + 3 steps).
+With `--gpus N > 1` and no torchrun environment, bench.py starts the N ranks itself (spawned children; the parent
+makes no GPU call).  `--dry-run` replaces the HIP model by a CPU stand-in on gloo, to test the launch plumbing without
+a GPU.  Rank 0 prints ONE JSON line.
+
+Live roofline: HIP events on the compute stream bracket every hot launch of the step, grouped into families
+(forward / dgrad / wgrad GEMMs, attention fwd/bwd, LayerNorm fwd/bwd), each launch carrying its algorithmic FLOPs and
+HBM bytes.  `roofline` reports the family that takes the most time; `roofline_families`
+reports all of them.  `traffic` is the measured HBM bytes of that family (rocprofv3 PMC passes committed under
+profiles/ for this exact workload), or null when no such profile exists.
+`cpu_baseline` times the repo's own host training step (train.py `time_steps`, VisionTransformer/_cpu.py) on all the
+cores this process may use: BASELINE config 1 exactly (ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 steps) and a bounded
+ViT-Base/16 224^2 fp32 sample whose images/s is `value`.
 """
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -29,6 +37,8 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16 = 2.5e15      # dense bf16 MFMA, MI355X (MI355X_MICROARCH.md chip table; no sparsity)
 PEAK_F32 = 157.3e12     # fp32 MFMA
+PEAK_HBM = 8.0e12       # HBM3E bytes/s
+METRIC = "images/sec fwd+bwd ViT-Base/16 224^2 bf16 (train step incl. AdamW); % MFMA roofline"
 
 
 def gflop_per_image(D, L, T, N, P, C, nc):
@@ -39,14 +49,19 @@ def gflop_per_image(D, L, T, N, P, C, nc):
     return (2 * pe + 3 * (L * block + head)) / 1e9
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes (profiles/, FETCH_SIZE with
-    the gfx950 x2 correction + WRITE_SIZE; tools/r2d.sh), or None."""
+def workload_key(args):
+    return f"{args.model}_{args.img}_b{args.batch}_{args.dtype}"
+
+
+def pmc_traffic(key, family):
+    """Measured HBM bytes per step of `family` for this workload (profiles/pmc_<key>.json, written by
+    tools/pmc_families.py from rocprofv3 PMC passes: FETCH_SIZE (x2 gfx950 correction) + WRITE_SIZE), or None."""
     try:
-        with open(os.path.join(ROOT, "profiles", "r2_qkv_fwd_pmc.json")) as f:
-            return int(json.load(f)["hbm_bytes_per_launch"])
-    except (OSError, KeyError, ValueError):
-        return None
+        with open(os.path.join(ROOT, "profiles", f"pmc_{key}.json")) as f:
+            fam = json.load(f)["families"][family]
+        return int(fam["hbm_bytes_per_step"]), fam
+    except (OSError, KeyError, ValueError, TypeError):
+        return None, None
 
 
 def gemm_peak(dev, n=8192, reps=5):
@@ -76,114 +91,188 @@ def gemm_peak(dev, n=8192, reps=5):
             "hipblaslt_tflops": round(flop / t_lib / 1e12, 1)}
 
 
-def cpu_baseline(model_name, img, nc, batch=8, warmup=1, steps=3):
-    from oracle import vit_oracle as O
-    threads = min(16, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(threads)
-    ocfg = O.make_config(model_name, img=img, batch=batch, num_classes=nc)
-    st = O.init_state(ocfg, seed=0)
-    opt = O.AdamWState(st, lr=1e-4)
-    x, y = O.synthetic_batch(ocfg)
-    t0 = None
-    for i in range(warmup + steps):
-        if i == warmup:
-            t0 = time.perf_counter()
-        _, loss, grads = O.loss_and_grads(st, x, y, ocfg, train=True, seed=i)
-        opt.step(st, grads)
-    dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/vit_oracle.py train step (fwd+CE+bwd+AdamW, dropout on), ViT-{model_name}/16 {img}^2 "
-                      f"fp32, batch {batch}, {warmup} warmup + {steps} timed steps, {threads} threads"}
+def log(msg):
+    """Progress on stderr (a long silent run looks hung to the GPU box's watchdog)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="base", choices=["tiny", "small", "base", "large"])
-    ap.add_argument("--img", type=int, default=224)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--classes", type=int, default=1000)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
-    args = ap.parse_args()
+def host_topology():
+    """Threads this process may use — the CPUs in its affinity mask, capped by the machine's OMP_NUM_THREADS share
+    when one is set (the GPU box exports 16 per GPU) — plus sockets / physical cores of the host (/proc/cpuinfo)."""
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(affinity, share) if share > 0 else affinity
+    sockets, cores = set(), set()
+    try:
+        phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":")[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":")[1].strip()
+                elif not line.strip() and phys is not None:
+                    sockets.add(phys)
+                    cores.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    return {"threads_used": threads, "affinity_cpus": affinity, "omp_num_threads": share or None,
+            "host_logical_cpus": os.cpu_count(), "sockets": len(sockets) or None, "physical_cores": len(cores) or None}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+
+def cpu_baseline(img, nc, budget_s=20.0):
+    """The repo's own CPU training step (train.py time_steps -> VisionTransformer/_cpu.py, torch.optim.AdamW) on every
+    core this process may use.  C1 exactly (ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 timed steps), then ViT-Base/16
+    img^2 fp32 B32: 1 warmup step, then as many timed steps (1-3) as fit in ~budget_s."""
+    import train as T
+    from VisionTransformer import config
+    topo = host_topology()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(topo["threads_used"])
+    try:
+        c1 = config.ViTConfig(3, 10, 16, 192, 16, 3, 12, "cpu", 8)
+        log(f"cpu baseline: C1 on {topo['threads_used']} threads")
+        s1, _ = T.time_steps(c1, steps=30, warmup=5, dev="cpu")
+        log(f"cpu baseline: C1 {s1 * 1e3:.1f} ms/step; ViT-B B32 warmup step")
+        cb = config.ViTConfig.preset("base", img_size=img, batch_size=32, num_classes=nc, precision=torch.float32,
+                                     device="cpu")
+        t0 = time.perf_counter()
+        T.time_steps(cb, steps=0, warmup=1, dev="cpu")
+        one = time.perf_counter() - t0
+        steps = int(max(1, min(3, budget_s // max(one, 1e-3))))
+        log(f"cpu baseline: ViT-B step {one:.1f} s; timing {steps} step(s)")
+        sb, _ = T.time_steps(cb, steps=steps, warmup=1, dev="cpu")
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(32 / sb, 3), "unit": "images/s", "cores": topo["threads_used"], "kind": "port",
+            "sample": f"repo train.py host step (VisionTransformer/_cpu.py fwd+CE+bwd + torch AdamW, dropout on), "
+                      f"ViT-Base/16 {img}^2 fp32 B32, 1 warmup + {steps} timed steps, "
+                      f"{topo['threads_used']} threads",
+            "topology": topo,
+            "c1": {"workload": "BASELINE config 1: ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 timed steps",
+                   "ms_per_step": round(s1 * 1e3, 3), "images_per_s": round(8 / s1, 3)}}
+
+
+class FamilyTimer:
+    """HIP events around every hot launch (engine.profile_hook), grouped by kernel family."""
+
+    def __init__(self):
+        self.open = {}
+        self.done = []          # (family, start, end, flop, bytes)
+
+    def __call__(self, fam, phase, flop=0.0, nbytes=0.0):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if phase == 0:
+            self.open[fam] = (ev, flop, nbytes)
+        else:
+            s, f, b = self.open.pop(fam)
+            self.done.append((fam, s, ev, f, b))
+
+    def summary(self, steps):
+        fams = {}
+        for fam, s, e, f, b in self.done:
+            d = fams.setdefault(fam, {"launches": 0, "time_s": 0.0, "flop": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["time_s"] += s.elapsed_time(e) / 1e3
+            d["flop"] += f
+            d["bytes"] += b
+        out = {}
+        for fam, d in fams.items():
+            t = max(d["time_s"], 1e-12)
+            out[fam] = {"launches_per_step": d["launches"] // steps, "ms_per_step": round(d["time_s"] / steps * 1e3, 3),
+                        "avg_launch_us": round(t / d["launches"] * 1e6, 2),
+                        "tflops": round(d["flop"] / t / 1e12, 2), "hbm_gbs_algorithmic": round(d["bytes"] / t / 1e9, 1),
+                        "flop_per_step": d["flop"] / steps, "bytes_per_step": d["bytes"] / steps}
+        return out
+
+
+def run(args, rank, world, local):
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
-    from VisionTransformer import config, vit
-    from VisionTransformer.optim import FusedAdamW, cross_entropy
+        dev = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    cfg = config.ViTConfig.preset(args.model, img_size=args.img, batch_size=args.batch, num_classes=args.classes,
-                                  precision=dtype, device="cpu")
-    torch.manual_seed(0)                       # identical init on every rank (reference init order, CPU RNG)
-    model = vit.VisionTransformer(cfg).to(dev).train()
-    if world > 1:
-        model.enable_data_parallel()
-    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
-    gen = torch.Generator().manual_seed(1234 + rank)
-    x = torch.randn(args.batch, 3, args.img, args.img, generator=gen).to(dev)
-    y = torch.randint(0, args.classes, (args.batch,), generator=torch.Generator().manual_seed(1235 + rank)).to(dev)
+    if args.dry_run:          # launch-plumbing stand-in: one small CPU GEMM + a gradient-sized all-reduce per step
+        w = torch.randn(256, 256)
+        g = torch.zeros(1 << 16)
 
-    eng = model.hip_engine
-    D, L, T, N = cfg.embedding_size, cfg.num_blocks, cfg.num_patches + 1, cfg.num_patches
-    M = args.batch * T
-    qkv_flop = 2.0 * M * 3 * D * D
-    events = []
+        def step():
+            y = (w @ w).sum()
+            if world > 1:
+                dist.all_reduce(g)
+            return y
+        D = L = T = N = 0
+        cfg = None
+    else:
+        from VisionTransformer import config, vit
+        from VisionTransformer.optim import FusedAdamW, cross_entropy
+        cfg = config.ViTConfig.preset(args.model, img_size=args.img, batch_size=args.batch, num_classes=args.classes,
+                                      precision=dtype, device="cpu")
+        torch.manual_seed(0)                       # identical init on every rank (reference init order, CPU RNG)
+        model = vit.VisionTransformer(cfg).to(dev).train()
+        if world > 1:
+            model.enable_data_parallel()
+        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+        gen = torch.Generator().manual_seed(1234 + rank)
+        x = torch.randn(args.batch, 3, args.img, args.img, generator=gen).to(dev)
+        y = torch.randint(0, args.classes, (args.batch,), generator=torch.Generator().manual_seed(1235 + rank)).to(dev)
+        D, L, T, N = cfg.embedding_size, cfg.num_blocks, cfg.num_patches + 1, cfg.num_patches
 
-    def hook(name, phase):
-        if name == "qkv_fwd":
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            events.append(ev)
+        def step():
+            logits = model(x)
+            loss = cross_entropy(logits, y)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            return loss
 
-    def step():
-        logits = model(x)
-        loss = cross_entropy(logits, y)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        opt.step()
-        return loss
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
+    log(f"rank {rank}/{world}: warmup {args.warmup} steps")
     for _ in range(args.warmup):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
+    log(f"rank {rank}/{world}: timing {args.steps} steps")
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    eng.profile_hook = hook
+    sync()
+    timer = None
+    if not args.dry_run and not args.no_roofline:
+        timer = FamilyTimer()
+        model.hip_engine.profile_hook = timer
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    eng.profile_hook = None
+    sync()
     if world > 1:
         dist.barrier()
+    sync()
+    t1 = time.perf_counter()
+    if timer is not None:
+        model.hip_engine.profile_hook = None
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
-    final_loss = loss.item()
-    kdur = [events[i].elapsed_time(events[i + 1]) / 1e3 for i in range(0, len(events) - 1, 2)]
-    kavg = sum(kdur) / max(len(kdur), 1)
+        elapsed = float(tt.item())
+    final_loss = float(loss.item())
+    log(f"rank {rank}/{world}: {elapsed / args.steps * 1e3:.2f} ms/step")
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         imgs = world * args.batch * args.steps / elapsed
-        gf = gflop_per_image(D, L, T, N, cfg.patch_size, 3, args.classes)
-        peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
         out = {
-            "metric": "images/sec fwd+bwd ViT-Base/16 224^2 bf16 (train step incl. AdamW); % MFMA roofline",
+            "metric": METRIC,
             "value": round(imgs, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -199,23 +288,94 @@ def main():
                                    f"(fwd+CE+bwd+AdamW), batch {args.batch}/GPU",
                        "model": f"vit_{args.model}_patch16_{args.img}", "global_batch": args.batch * world,
                        "seq_len": T, "parallelism": f"dp{world}"},
-            "step_mfma_frac": round(imgs * gf * 1e9 / (world * peak), 4),
-            "gflop_per_image": round(gf, 3),
-            "final_loss": round(final_loss, 4),
-            "roofline": {"bound": "mfma", "kernel": "gemm_bf16_v4<true,true,bf16,0> (fused QKV projection forward)",
-                         "achieved": round(qkv_flop / kavg / 1e12, 2) if kavg > 0 else None,
-                         "peak": peak / 1e12, "unit": "TFLOP/s",
-                         "frac": round(qkv_flop / kavg / peak, 4) if kavg > 0 else None,
-                         "flop_per_launch": qkv_flop, "avg_launch_us": round(kavg * 1e6, 2),
-                         "launches_timed": len(kdur), "traffic": pmc_traffic(),
-                         "traffic_source": "profiles/r2_qkv_fwd_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"},
-            "measured_gemm_peak": None if args.no_gemm_peak else gemm_peak(dev),
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.model, args.img, args.classes)
+        if args.dry_run:
+            out["dry_run"] = True
+            out["data"] = "dry run: CPU stand-in step on gloo, no HIP model (launch plumbing only)"
+        else:
+            gf = gflop_per_image(D, L, T, N, cfg.patch_size, 3, args.classes)
+            peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
+            out["step_mfma_frac"] = round(imgs * gf * 1e9 / (world * peak), 4)
+            out["gflop_per_image"] = round(gf, 3)
+            out["final_loss"] = round(final_loss, 4)
+            if timer is not None:
+                fams = timer.summary(args.steps)
+                dom = max(fams, key=lambda f: fams[f]["ms_per_step"])
+                d = fams[dom]
+                key = workload_key(args)
+                traffic, pmc = pmc_traffic(key, dom)
+                if dom.startswith("gemm") or dom.startswith("attn"):
+                    ach, pk, unit, bound = d["tflops"], peak / 1e12, "TFLOP/s", "mfma"
+                else:
+                    ach, pk, unit, bound = d["hbm_gbs_algorithmic"], PEAK_HBM / 1e9, "GB/s", "hbm"
+                out["roofline"] = {
+                    "bound": bound, "family": dom, "achieved": ach, "peak": pk, "unit": unit,
+                    "frac": round(ach / pk, 4), "traffic": traffic,
+                    "traffic_unit": "HBM bytes per step for this family (rocprofv3 PMC)",
+                    "algorithmic_bytes_per_step": int(d["bytes_per_step"]),
+                    "traffic_source": f"profiles/pmc_{key}.json" if traffic is not None else None,
+                    "ms_per_step": d["ms_per_step"], "launches_per_step": d["launches_per_step"],
+                    "avg_launch_us": d["avg_launch_us"],
+                    "kernels": {"gemm_wgrad": "gemm_bf16_v4<false,false,float,EPI_SLAB> + splitk_reduce",
+                                "gemm_fwd": "gemm_bf16_v4<true,true,bf16,*>", "gemm_dgrad": "gemm_bf16_v4<true,false,*>",
+                                "attn_fwd": "attn_fwd_fused / attn_fwd_mfma", "attn_bwd": "attn_bwd_fused / tiled",
+                                "ln_fwd": "ln_fwd_kernel", "ln_bwd": "ln_bwd_kernel"}.get(dom, dom)}
+                for f, v in fams.items():
+                    pk_f = peak if (f.startswith("gemm") or f.startswith("attn")) else None
+                    v["mfma_frac"] = round(v["tflops"] * 1e12 / peak, 4) if pk_f else None
+                    v["hbm_frac_algorithmic"] = round(v["hbm_gbs_algorithmic"] * 1e9 / PEAK_HBM, 4)
+                    del v["flop_per_step"], v["bytes_per_step"]
+                out["roofline_families"] = fams
+            if not args.no_gemm_peak:
+                log("measured GEMM peak")
+                out["measured_gemm_peak"] = gemm_peak(dev)
+        if world == 1 and not args.no_cpu_baseline and not args.dry_run:
+            out["cpu_baseline"] = cpu_baseline(args.img, args.classes)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _spawned(rank, args, world, port):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(args, rank, world, rank)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="base", choices=["tiny", "small", "base", "large"])
+    ap.add_argument("--img", type=int, default=224)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
+    ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events (profiling runs)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo stand-in step: tests rank launch without a GPU")
+    args = ap.parse_args(argv)
+
+    if "WORLD_SIZE" in os.environ:           # launched by torchrun: one rank per process
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
+        run(args, int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0")))
+    elif args.gpus > 1:                      # start the ranks here; this parent makes no GPU call
+        import torch.multiprocessing as mp
+        mp.start_processes(_spawned, args=(args, args.gpus, _free_port()), nprocs=args.gpus, start_method="spawn")
+    else:
+        run(args, 0, 1, 0)
 
 
 if __name__ == "__main__":

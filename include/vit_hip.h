@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 3
+#define VIT_ABI_VERSION 4
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1 } vit_dtype;
@@ -91,6 +91,10 @@ int vit_gemm(const vit_gemm_desc* d, void* stream);
  * ------------------------------------------------------------------------------------------------------------ */
 int vit_im2col(const void* x, int32_t x_dtype, void* cols, int32_t dtype, int64_t B, int64_t C, int64_t H,
                int64_t W, int64_t P, void* stream);
+/* vit_col2im: the inverse permutation of vit_im2col (k = s = P): x[B][C][H][W] (x_dtype) <- cols[B*N][C*P*P] (dtype).
+ * Used for the input-image gradient (conv dgrad, vit.py:21-28 backward) when the caller's input requires grad. */
+int vit_col2im(const void* cols, int32_t dtype, void* x, int32_t x_dtype, int64_t B, int64_t C, int64_t H, int64_t W,
+               int64_t P, void* stream);
 int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, int64_t B, int64_t T, int64_t D,
                   void* stream);
 
@@ -119,13 +123,18 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, 
  *   lse[B][H][T] (natural log of the row softmax denominator, scaled-logit domain) saved for backward;
  *   probs [B][H][T][T] f32 optional (the `.attention_probs` side attribute, transformer.py:48).
  * bf16 & hd == 64: flash-style MFMA kernels (K/V tiles in LDS, online softmax); otherwise a generic VALU kernel.
+ * o32 (bf16 only, optional): the forward also stores O unrounded, [B*T][D] f32, and the backward takes it to form
+ *   delta = rowsum(dO * O) exactly in fp32.  Under the reference's x sqrt(hd) logit scale most softmax rows saturate,
+ *   dS = P (dP - delta) becomes a small difference, and delta from the bf16 O dominates the Q / K gradients; with
+ *   o32 == NULL the backward uses the bf16 O (standard flash-attention practice, cheaper).
  * bwd: dqkv[B*T][3*D]; workspace = vit_attn_bwd_workspace_bytes.
  * ------------------------------------------------------------------------------------------------------------ */
-int vit_attn_fwd(const void* qkv, void* o, float* lse, float* probs, int64_t B, int64_t T, int64_t H, int64_t hd,
-                 float scale, int32_t dtype, void* stream);
+int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, float* probs, int64_t B, int64_t T, int64_t H,
+                 int64_t hd, float scale, int32_t dtype, void* stream);
 int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
-int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, const float* lse, void* dqkv, int64_t B,
-                 int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace, void* stream);
+int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d_o, const float* lse, void* dqkv,
+                 int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace,
+                 void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------
  * Reductions / elementwise.
@@ -154,6 +163,20 @@ int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream);
 int vit_gelu_bwd(const float* x, const float* dy, float* dx, int64_t n, void* stream);
 int vit_softmax_xent(const float* logits, const int64_t* labels, int64_t rows, int64_t classes, float* loss,
                      float* dlogits, float* workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------------------------
+ * Image pipeline of the training loader (train.py:151-155: convert('RGB') -> transforms.Resize((S, S)) ->
+ * ToTensor; BrainTumorDataset.py:35-39 / CIFAR10 :157-159 feed it PIL images).  A batch of raw uint8 HWC images of
+ * any sizes (ragged allowed), packed into one byte buffer `src`, described by meta[B][4] = (byte offset, H, W, C)
+ * (int64, DEVICE memory; C in {1: L, 2: LA, 3: RGB, 4: RGBA} -> RGB as PIL converts), becomes out[B][3][S_h][S_w]
+ * (VIT_F32 or VIT_BF16) = PIL-bilinear-resized pixel / 255, bit-exact with Pillow's 8-bit two-pass resampler.
+ *   vit_resize_ksize: taps per output sample for one axis (in_size -> out_size); pass the max over the batch and axes.
+ *   workspace: vit_resize_workspace_bytes(B, S_h, S_w, ksize) bytes (per-image coefficient tables).
+ * ------------------------------------------------------------------------------------------------------------ */
+int vit_resize_ksize(int64_t in_size, int64_t out_size);
+int64_t vit_resize_workspace_bytes(int64_t B, int64_t out_h, int64_t out_w, int64_t ksize);
+int vit_resize_to_tensor(const void* src, const int64_t* meta, int64_t B, int64_t out_h, int64_t out_w, int64_t ksize,
+                         void* out, int32_t out_dtype, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------
  * Optimizer (train.py:66,96: torch.optim.AdamW(lr, weight_decay=1e-4), betas (0.9, 0.999), eps 1e-8) as ONE

@@ -41,14 +41,111 @@ def test_state_dict_roundtrip_with_oracle_keys():
         assert torch.equal(v, st[k])
 
 
-def test_cpu_forward_fails_loudly():
+def test_host_path_matches_reference_goldens(golden_dir):
+    """CPU model + CPU input runs the package's own host path (VisionTransformer/_cpu.py: fused QKV GEMM + batched
+    attention with the multiplied sqrt(hd) scale), never the oracle: G1 micro logits / loss / every gradient."""
+    import numpy as np
+    g = np.load(os.path.join(golden_dir, "micro.npz"))
+    torch.manual_seed(0)
+    m = vit.VisionTransformer(_cfg("micro")).eval()
+    x, y = torch.from_numpy(g["x"]), torch.from_numpy(g["y"])
+    logits = m(x)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    np.testing.assert_allclose(logits.detach().numpy(), g["logits"], atol=1e-5, rtol=0)
+    assert abs(loss.item() - float(g["loss"])) < 1e-6
+    for k, p in m.named_parameters():
+        ref = g["grad/" + k]
+        assert np.abs(p.grad.numpy() - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max()), k
+
+
+def test_host_path_c1_and_module_api(golden_dir):
+    """BASELINE config 1 dims (ViT-Tiny/16 64^2 B8) on the host path vs the reference's fp32 logits (G4), and the
+    module-level API (Head returns (out, wei); MultiHeadAttention sets attention_probs) on CPU tensors."""
+    import numpy as np
+    g = np.load(os.path.join(golden_dir, "tiny.npz"))
+    torch.manual_seed(0)
+    m = vit.VisionTransformer(_cfg("tiny")).eval()
+    x, _ = O.synthetic_batch(O.make_config("tiny", img=64, batch=8))
+    with torch.no_grad():
+        logits = m(x)
+    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=2e-4, rtol=0)
+    gk = np.load(os.path.join(golden_dir, "ops.npz"))
+    head = transformer.Head(16, 64, 5)
+    with torch.no_grad():
+        head.query.weight.copy_(torch.from_numpy(gk["head/wq"]))
+        head.key.weight.copy_(torch.from_numpy(gk["head/wk"]))
+        head.value.weight.copy_(torch.from_numpy(gk["head/wv"]))
+    out, wei = head(torch.from_numpy(gk["head/x"]))
+    np.testing.assert_allclose(out.detach().numpy(), gk["head/out"], atol=1e-5)
+    np.testing.assert_allclose(wei.numpy(), gk["head/wei"], atol=1e-6)
+    mh = transformer.MultiHeadAttention(2, 8, 16, 5).eval()
+    mh(torch.randn(3, 5, 16))
+    assert tuple(mh.attention_probs.shape) == (3, 2, 5, 5)
+
+
+def test_device_ops_refuse_host_tensors():
+    """The HIP ops never compute on host tensors (no CPU fallback inside the device path)."""
+    from VisionTransformer import _ops
+    a = torch.zeros(4, 4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        _ops.gemm(a, a, a, 4, 4, 4, 4, 4, 4)
+
+
+def test_missing_library_raises(monkeypatch):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/libvit_hip.so")
+    with pytest.raises(_lib.HipLibraryError, match="no CPU fallback"):
+        _lib.load()
+
+
+def test_deepcopy_and_pickle_drop_the_engine():
+    import copy
+    import pickle
     torch.manual_seed(0)
     m = vit.VisionTransformer(_cfg("micro"))
-    with pytest.raises(RuntimeError, match="ROCm device"):
-        m(torch.randn(4, 3, 32, 32))
-    blk = m.transformer_encoder.blocks[0]
-    with pytest.raises(RuntimeError, match="ROCm device"):
-        blk(torch.randn(4, 5, 64))
+    eng = m.hip_engine
+    eng._build(m, torch.device("cpu"))
+    for clone in (copy.deepcopy(m), pickle.loads(pickle.dumps(m))):
+        assert clone._engine is None and clone.hip_engine is not eng and clone.hip_engine.model_ref() is clone
+        assert all(_engine.shadow_of(p) is None for p in clone.parameters())
+        for (k, a), b in zip(m.state_dict().items(), clone.state_dict().values()):
+            assert torch.equal(a, b) and a.data_ptr() != b.data_ptr(), k
+
+
+def test_train_py_host_path_runs_c1_loop(tmp_path):
+    """train.py --device cpu: the reference loop (train.py:89-102) with checkpoint + resume on the host path."""
+    import subprocess
+    import sys
+    cmd = [sys.executable, os.path.join(ROOT, "vision-transformer_amd", "train.py"), "--device", "cpu", "--model",
+           "tiny", "--img", "64", "--batch", "8", "--steps", "3", "--train-size", "32", "--test-size", "16",
+           "--epochs", "1", "--workers", "0", "--threads", "2", "--checkpoint-dir", str(tmp_path / "ck"),
+           "--log-dir", str(tmp_path / "logs")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert sorted(os.listdir(tmp_path / "ck")) == ["0.pt", "1.pt"]
+    ck = torch.load(tmp_path / "ck" / "1.pt", weights_only=True)
+    assert ck["step"] == 6 and "transformer_encoder.blocks.11.multi_head.heads.2.query.weight" in ck["model_state_dict"]
+    r = subprocess.run(cmd[:-4] + ["--bench", "--steps", "2", "--warmup", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["device"] == "cpu" and line["steps"] == 2 and line["ms_per_step"] > 0
+
+
+def test_bench_spawns_ranks_dry_run():
+    """`bench.py --gpus 2` without torchrun starts 2 ranks itself (spawn; the parent makes no GPU call) and rank 0
+    prints one JSON line with n_gpus = 2, dp2, global batch 512 (the driver's --gpus N contract)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 512
+    assert out["dry_run"] is True and out["value"] > 0
 
 
 def test_library_exports_every_header_symbol():
@@ -89,7 +186,7 @@ def test_engine_layout_views():
             assert gv[id(head.query.weight)].data_ptr() == fused[h * hd].data_ptr()
             assert gv[id(head.key.weight)].data_ptr() == fused[D + h * hd].data_ptr()
             assert gv[id(head.value.weight)].data_ptr() == fused[2 * D + h * hd].data_ptr()
-            assert head.query.weight._vit_shadow.data_ptr() == eng.ww[f"{l}.qkv_w"][h * hd].data_ptr()
+            assert _engine.shadow_of(head.query.weight).data_ptr() == eng.ww[f"{l}.qkv_w"][h * hd].data_ptr()
     # buckets: head | block L-1 | ... | block 0 | embedding, contiguous and ordered
     rngs = [eng.head_range] + [eng.block_range[l] for l in reversed(range(2))] + [eng.embed_range]
     for (a0, b0), (a1, b1) in zip(rngs, rngs[1:]):

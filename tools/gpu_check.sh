@@ -11,7 +11,10 @@ export TMPDIR=/tmp
 fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; }
 for s in $STEPS; do
   case $s in
-    tests) timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > "$OUT/tests.log" 2>&1 ;;
+    tests) timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 \
+             --timeout-method thread > "$OUT/tests.log" 2>&1 ;;
+    newtests) timeout -k 10 600 python -u -m pytest tests/test_gpu_dropin.py -v -m gpu -p no:cacheprovider \
+             --timeout 300 --timeout-method thread > "$OUT/newtests.log" 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

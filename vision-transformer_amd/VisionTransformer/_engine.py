@@ -24,9 +24,19 @@ import weakref
 
 import torch
 import torch.distributed as dist
+from torch.utils.weak import WeakIdKeyDictionary
 
 from . import _lib, _ops
 from ._ops import ACT_NONE, ACT_RELU
+
+# parameter -> its compute-dtype shadow view (refreshed by FusedAdamW's kernel).  Kept beside the parameters, not as
+# attributes on them, so models stay picklable / deep-copyable (torch.save(model), EMA snapshots).
+SHADOWS = WeakIdKeyDictionary()
+
+
+def shadow_of(p):
+    return SHADOWS.get(p)
+
 
 DROPOUT_P = 0.2          # transformer.py:35,53 (config.dropout is stored but unused by the reference)
 LN_EPS = 1e-5
@@ -77,7 +87,8 @@ def head_split_for(m, n, k):
 
 class Tape:
     """Activations saved by a training forward."""
-    __slots__ = ("B", "cols", "blocks", "z", "u", "gz", "zn", "mh", "rh", "seed", "training")
+    __slots__ = ("B", "cols", "blocks", "z", "u", "gz", "zn", "mh", "rh", "seed", "training", "x_shape", "x_dtype",
+                 "x_grad")
 
 
 class Engine:
@@ -103,7 +114,9 @@ class Engine:
         self._ptr_sig = None
         self._ver_sig = None
         self.stats = {"packs": 0}
-        self.profile_hook = None          # callable(name, phase) around named launches (bench.py HIP events)
+        # callable(family, phase, flop, nbytes) around the hot launches (bench.py's live HIP-event roofline):
+        # phase 0 before the launch with its algorithmic FLOPs / HBM bytes, phase 1 after it, same stream
+        self.profile_hook = None
         # weight-gradient GEMMs on a side stream (VIT_CONCURRENT_WGRAD=1).  Off by default: measured on ViT-B/16
         # B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms/step).
         self.concurrent_wgrad = os.environ.get("VIT_CONCURRENT_WGRAD", "0") == "1"
@@ -213,12 +226,17 @@ class Engine:
                 gv = self.gw[key].view(p.shape)
                 sv = self.ww[key].view(p.shape) if key in self.ww else None
             self.grad_views.append((p, gv))
-            p._vit_shadow = sv
-            p._vit_engine = weakref.ref(self)
+            SHADOWS[p] = sv
             if sv is not None:
                 self.pack_entries.append((p, sv))
         self.params = params
         self.param_list = list(params.values())
+        # which parameters feed each gradient region (a fused QKV region serves 3H per-head parameters)
+        self.owners = {}
+        for name, p in params.items():
+            l, _, short = name.partition(".") if "." in name else ("", "", name)
+            key = f"{l}.qkv_w" if (short and short[0] in "qkv" and short[1:].isdigit()) else name
+            self.owners.setdefault(key, []).append(p)
         self.device = device
         self._pack_table = None
         self._ptr_sig = self._pointer_signature()
@@ -232,6 +250,9 @@ class Engine:
 
     def ensure_ready(self, device):
         model = self.model_ref()
+        if model is None or getattr(model, "_engine", None) is not self:
+            raise RuntimeError("this engine does not belong to the model it is called for (copied engine?); "
+                               "models must build their own engine (VisionTransformer.hip_engine)")
         if self.params is None or self.device != device or self._pointer_signature() != self._ptr_sig:
             self._build(model, device)
         ver = self._version_signature()
@@ -269,15 +290,24 @@ class Engine:
             self._wstream = torch.cuda.Stream(device=self.device)
         return self._wstream
 
-    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta, side=None):
+    def _mark(self, fam, phase, flop=0.0, nbytes=0.0):
+        h = self.profile_hook
+        if h is not None:
+            h(fam, phase, flop, nbytes)
+
+    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta, side=None, fam=None):
         """out[m][n] (+)= sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K.  With `side` it
         runs on that stream after everything already enqueued on the current one."""
         split = split_k_for(m, n, k, dy.dtype)
         need = split * m * n * 4 if split > 1 else 0
         if side is None:
             ws = self._workspace(need) if split > 1 else None
+            if fam:
+                self._mark(fam, 0, 2.0 * m * n * k, (m + n) * k * dy.element_size() + m * n * 4 * (1 + (beta != 0)))
             _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
                       split_k=split, workspace=ws)
+            if fam:
+                self._mark(fam, 1)
             return
         side.wait_stream(torch.cuda.current_stream(self.device))
         ws = None
@@ -306,16 +336,18 @@ class Engine:
         _ops.colsum(x, rows, cols, ld, out, beta=beta)
 
     def _attach_grads(self):
-        """Expose the flat gradient buffer as param.grad; returns beta (1.0 accumulate / 0.0 overwrite)."""
-        live = [p.grad is not None and p.grad.data_ptr() == gv.data_ptr() for p, gv in self.grad_views]
+        """Expose the flat gradient buffer as param.grad of every parameter that requires grad (frozen ones keep
+        .grad untouched, as autograd would); returns beta (1.0 accumulate / 0.0 overwrite)."""
+        views = [(p, gv) for p, gv in self.grad_views if p.requires_grad]
+        live = [p.grad is not None and p.grad.data_ptr() == gv.data_ptr() for p, gv in views]
         if all(live):
             return 1.0
-        if not any(p.grad is not None for p, _ in self.grad_views):
-            for p, gv in self.grad_views:
+        if not any(p.grad is not None for p, _ in views):
+            for p, gv in views:
                 p.grad = gv
             return 0.0
         # mixed: zero the regions whose grad was dropped/replaced, keep accumulating elsewhere
-        for (p, gv), ok in zip(self.grad_views, live):
+        for (p, gv), ok in zip(views, live):
             if not ok:
                 if p.grad is not None:
                     gv.copy_(p.grad)
@@ -348,41 +380,58 @@ class Engine:
             x = x.float()
         D, T, N, H, hd, L, dt = self.D, self.T, self.N, self.H, self.hd, self.L, self.dtype
         M = B * T
+        es = 2 if dt == torch.bfloat16 else 4
         prm = self.params
+        mk = self._mark
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training else 0
         tape = Tape() if save else None
 
         cols = _ops.im2col(x, self.P, dt)                                             # vit.py:21-29 as GEMM
         xcur = torch.empty(M, D, dtype=dt, device=x.device)
+        mk("gemm_fwd", 0, 2.0 * B * N * D * self.CPP, (B * N + D) * self.CPP * es + B * N * D * es)
         _ops.gemm(cols, self.ww["conv_w"], xcur, B * N, D, self.CPP, self.CPP, self.CPP, D, bias=prm["conv_b"],
                   res=prm["pos"].view(T, D), ldres=D, res_rowmod=N, out_group=(N, T))  # + pos, rows -> b*T+n
+        mk("gemm_fwd", 1)
         _ops.embed_cls(prm["cls"], prm["pos"], xcur, B, T, D)                           # CLS appended LAST (vit.py:41)
         blocks = []
         for l in range(L):
             blk = model.transformer_encoder.blocks[l]
             x_in = xcur
+            ln_b = 2 * M * D * es + 8 * M
+            mk("ln_fwd", 0, 0.0, ln_b)
             a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
-            hook = self.profile_hook
-            if hook:
-                hook("qkv_fwd", 0)
+            mk("ln_fwd", 1)
+            mk("gemm_fwd", 0, 2.0 * M * 3 * D * D, (M * D + 3 * D * D + 3 * M * D) * es)
             qkv = _ops.linear(a1, self.ww[f"{l}.qkv_w"])                                # 3H heads' K/Q/V in one GEMM
-            if hook:
-                hook("qkv_fwd", 1)
+            mk("gemm_fwd", 1)
             probs = None
             if want_probs:
                 probs = torch.empty(B, H, T, T, dtype=torch.float32, device=x.device)
-            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs)
+            # training forward in bf16: also keep O unrounded for the backward's exact delta (see vit_hip.h)
+            o32 = torch.empty(M, D, dtype=torch.float32, device=x.device) if (save and dt != torch.float32) else None
+            mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
+                                                                                         else 0))
+            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
+            mk("attn_fwd", 1)
             blk.multi_head.attention_probs = probs
             x_mid = torch.empty(M, D, dtype=dt, device=x.device)
+            mk("gemm_fwd", 0, 2.0 * M * D * D, (3 * M * D + D * D) * es)
             _ops.gemm(o, self.ww[f"{l}.proj_w"], x_mid, M, D, D, D, D, D, bias=prm[f"{l}.proj_b"], res=x_in,
                       ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 0))
+            mk("gemm_fwd", 1)
+            mk("ln_fwd", 0, 0.0, ln_b)
             a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
+            mk("ln_fwd", 1)
+            mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 4 * M * D) * es)
             h = _ops.linear(a2, self.ww[f"{l}.fc1_w"], bias=prm[f"{l}.fc1_b"], act=ACT_RELU)
+            mk("gemm_fwd", 1)
             x_out = torch.empty(M, D, dtype=dt, device=x.device)
+            mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (4 * M * D + 4 * D * D + 2 * M * D) * es)
             _ops.gemm(h, self.ww[f"{l}.fc2_w"], x_out, M, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
                       res=x_mid, ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 1))
+            mk("gemm_fwd", 1)
             if save:
-                blocks.append((x_in, a1, m1, r1, qkv, o, lse, x_mid, a2, m2, r2, h))
+                blocks.append((x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h))
             xcur = x_out
         # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
         z = torch.empty(B, D, dtype=torch.float32, device=x.device)
@@ -393,6 +442,7 @@ class Engine:
         logits = self._head_linear(zn, prm["h3_w"], prm["h3_b"])
         if save:
             tape.B, tape.cols, tape.blocks = B, cols, blocks
+            tape.x_shape, tape.x_dtype = tuple(x.shape), x.dtype
             tape.z, tape.u, tape.gz, tape.zn, tape.mh, tape.rh = z, u, gz, zn, mh, rh
             tape.seed, tape.training = seed, training
         return logits, tape
@@ -420,6 +470,8 @@ class Engine:
                 self._works.append((w, (a, b)))
 
     def _finish_buckets(self):
+        if not self._works:
+            return
         world = dist.get_world_size(self.ddp_group) if self.ddp_enabled else 1
         for w, rng in self._works:
             w.wait()
@@ -432,16 +484,28 @@ class Engine:
         B = tape.B
         M = B * T
         prm, gw = self.params, self.gw
+        es = 2 if dt == torch.bfloat16 else 4
+        mk = self._mark
         # decided at backward time: the reference calls zero_grad(set_to_none=True) between forward and backward
         beta = self._attach_grads()
+        req = {k: any(p.requires_grad for p in ps) for k, ps in self.owners.items()}
+        # the backward stops at the first block below which nothing (parameters, input image) needs a gradient
+        below = tape.x_grad or any(req[k] for k in ("conv_w", "conv_b", "cls", "pos"))
+        need_from = {}
+        for l in range(L):
+            below = below or any(req[f"{l}.{n}"] for n in ("qkv_w", "proj_w", "proj_b", "fc1_w", "fc1_b", "fc2_w",
+                                                           "fc2_b", "ln1_w", "ln1_b", "ln2_w", "ln2_b"))
+            need_from[l] = below
         dev = dlogits.device
         dlogits = dlogits.contiguous().float()
         nc = self.nc
         # ---- head (fp32)
         dzn = torch.empty(B, 4 * D, dtype=torch.float32, device=dev)
         self._head_gemm(dlogits, prm["h3_w"], dzn, B, 4 * D, nc, nc, 4 * D, 4 * D, b_kcontig=False)
-        self._wgrad(dlogits, tape.zn, gw["h3_w"], nc, 4 * D, B, nc, 4 * D, beta)
-        self._colsum(dlogits, B, nc, nc, gw["h3_b"], beta)
+        if req["h3_w"]:
+            self._wgrad(dlogits, tape.zn, gw["h3_w"], nc, 4 * D, B, nc, 4 * D, beta)
+        if req["h3_b"]:
+            self._colsum(dlogits, B, nc, nc, gw["h3_b"], beta)
         dgz = torch.empty_like(tape.gz)
         part = _ops.layernorm_bwd(dzn, tape.gz, prm["hln_w"], tape.mh, tape.rh, dgz)
         self._colsum(part[0], part.shape[1], 4 * D, 4 * D, gw["hln_w"], beta)
@@ -449,9 +513,14 @@ class Engine:
         du = _ops.gelu_bwd(tape.u, dgz)
         dz = torch.empty(B, D, dtype=torch.float32, device=dev)
         self._head_gemm(du, prm["h0_w"], dz, B, D, 4 * D, 4 * D, D, D, b_kcontig=False)
-        self._wgrad(du, tape.z, gw["h0_w"], 4 * D, D, B, 4 * D, D, beta)
-        self._colsum(du, B, 4 * D, 4 * D, gw["h0_b"], beta)
+        if req["h0_w"]:
+            self._wgrad(du, tape.z, gw["h0_w"], 4 * D, D, B, 4 * D, D, beta)
+        if req["h0_b"]:
+            self._colsum(du, B, 4 * D, 4 * D, gw["h0_b"], beta)
         self._bucket_ready(self.head_range)
+        if not need_from[L - 1]:
+            self._finish_buckets()
+            return None
         # ---- d(encoder output): only token-0 rows are nonzero
         dx = torch.zeros(M, D, dtype=dt, device=dev)
         _ops.copy2d(dz, D, dx, T * D, B, D)
@@ -463,63 +532,118 @@ class Engine:
         side = self._side_stream()
         g1_summed = False          # block L-1's fc2 bias gradient: g1 comes from the head (plain column sum below)
         for l in reversed(range(L)):
-            x_in, a1, m1, r1, qkv, o, lse, x_mid, a2, m2, r2, h = tape.blocks[l]
+            if not need_from[l]:
+                break
+            x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h = tape.blocks[l]
             # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
-            self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side)
+            if req[f"{l}.fc2_w"]:
+                self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side, "gemm_wgrad")
             if not g1_summed:
                 self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta)
             dh = torch.empty(M, 4 * D, dtype=dt, device=dev)
             dh_part = torch.empty(_ops.colsum_part_rows(M), 4 * D, dtype=torch.float32, device=dev)
             # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
+            mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 8 * M * D) * es)
             _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=h,
                       ldaux=4 * D, colsum_part=dh_part)
+            mk("gemm_dgrad", 1)
             _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
-            self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, M, 4 * D, D, beta, side)
+            if req[f"{l}.fc1_w"]:
+                self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, M, 4 * D, D, beta, side, "gemm_wgrad")
             da2 = torch.empty(M, D, dtype=dt, device=dev)
+            mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (4 * M * D + 4 * D * D + M * D) * es)
             _ops.gemm(dh, self.ww[f"{l}.fc1_w"], da2, M, D, 4 * D, 4 * D, D, D, b_kcontig=False)
+            mk("gemm_dgrad", 1)
             dx_mid = torch.empty(M, D, dtype=dt, device=dev)
             g0 = torch.empty(M, D, dtype=dt, device=dev) if tape.training else None
             # ln2 backward + residual add + dropout backward of the MHA branch; its third partial set is the column
             # sums of g0 as stored = the proj bias gradient
+            mk("ln_bwd", 0, 0.0, (3 + 1 + (g0 is not None)) * M * D * es + 8 * M)
             part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx,
                                       drop_out=g0, drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l, 0), osum=True)
+            mk("ln_bwd", 1)
             _ops.colsum_finish(part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta=beta)
             if g0 is None:
                 g0 = dx_mid
             # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
-            self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta, side)
+            if req[f"{l}.proj_w"]:
+                self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta, side, "gemm_wgrad")
             do = torch.empty(M, D, dtype=dt, device=dev)
+            mk("gemm_dgrad", 0, 2.0 * M * D * D, (2 * M * D + D * D) * es)
             _ops.gemm(g0, self.ww[f"{l}.proj_w"], do, M, D, D, D, D, D, b_kcontig=False)
+            mk("gemm_dgrad", 1)
+            mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 8 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
+                                                                                          else 0))
             dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
-                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)))
-            self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side)
+                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32)
+            mk("attn_bwd", 1)
+            if req[f"{l}.qkv_w"]:
+                self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
             da1 = torch.empty(M, D, dtype=dt, device=dev)
+            mk("gemm_dgrad", 0, 2.0 * M * 3 * D * D, (3 * M * D + 3 * D * D + M * D) * es)
             _ops.gemm(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
+            mk("gemm_dgrad", 1)
             dx_in = torch.empty(M, D, dtype=dt, device=dev)
             g1n = torch.empty(M, D, dtype=dt, device=dev) if (tape.training and l > 0) else None
             # ln1 backward; for l > 0 its third partial set is the column sums of the next g1 (g1n, or dx_in in eval)
             # = the fc2 bias gradient of block l-1
+            mk("ln_bwd", 0, 0.0, (3 + 1 + (g1n is not None)) * M * D * es + 8 * M)
             part = _ops.layernorm_bwd(da1, x_in, prm[f"{l}.ln1_w"], m1, r1, dx_in, dres=dx_mid, drop_out=g1n,
                                       drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l - 1, 1) if l > 0 else 0,
                                       osum=l > 0)
+            mk("ln_bwd", 1)
             outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if l > 0 else [])
             _ops.colsum_finish(part, outs, beta=beta)
             g1_summed = l > 0
             self._bucket_ready(self.block_range[l], side)
             dx = dx_in
             g1 = g1n if g1n is not None else dx_in
-        # ---- embedding (vit.py:39-42): dx = d(x0) [B*T, D]
-        _ops.copy2d(dx[N:], T * D, gw["cls"].view(B, D), D, B, D, beta=beta)           # CLS row of every image
-        self._colsum(dx, B, T * D, T * D, gw["pos"].view(-1), beta)                     # pos: sum over the batch
-        dpatch = torch.empty(B * N, D, dtype=dt, device=dev)
-        _ops.copy2d(dx, D, dpatch, D, B * N, D, group=(N, T))
-        self._colsum(dpatch, B * N, D, D, gw["conv_b"], beta)
-        self._wgrad(dpatch, tape.cols, gw["conv_w"], D, self.CPP, B * N, D, self.CPP, beta, side)
+        dimg = None
+        if need_from[0]:
+            # ---- embedding (vit.py:39-42): dx = d(x0) [B*T, D]
+            if req["cls"]:
+                _ops.copy2d(dx[N:], T * D, gw["cls"].view(B, D), D, B, D, beta=beta)       # CLS row of every image
+            if req["pos"]:
+                self._colsum(dx, B, T * D, T * D, gw["pos"].view(-1), beta)                 # pos: sum over the batch
+            dpatch = torch.empty(B * N, D, dtype=dt, device=dev)
+            _ops.copy2d(dx, D, dpatch, D, B * N, D, group=(N, T))
+            if req["conv_b"]:
+                self._colsum(dpatch, B * N, D, D, gw["conv_b"], beta)
+            if req["conv_w"]:
+                self._wgrad(dpatch, tape.cols, gw["conv_w"], D, self.CPP, B * N, D, self.CPP, beta, side,
+                            "gemm_wgrad")
+            if tape.x_grad:                   # input-image gradient: conv dgrad = dpatch W, scattered back (col2im)
+                dcols = torch.empty(B * N, self.CPP, dtype=dt, device=dev)
+                _ops.gemm(dpatch, self.ww["conv_w"], dcols, B * N, self.CPP, D, D, self.CPP, self.CPP,
+                          b_kcontig=False)
+                dimg = torch.empty(tape.x_shape, dtype=tape.x_dtype, device=dev)
+                _ops.col2im(dcols, dimg, self.P)
         self._bucket_ready(self.embed_range, side)
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)      # every weight gradient is in G before the step
-        if self._works:
-            self._finish_buckets()
+        self._finish_buckets()
+        return dimg
+
+    def run_param_hooks(self):
+        """Parameter hooks after the fused backward (autograd's AccumulateGrad never runs for these parameters):
+        `register_hook` hooks see the gradient and may replace it, then `register_post_accumulate_grad_hook`
+        hooks run on the parameter — each once per backward, in registration order."""
+        for p, gv in self.grad_views:
+            if not p.requires_grad or p.grad is None:
+                continue
+            pre = p._backward_hooks
+            if pre:
+                g = p.grad
+                for fn in pre.values():
+                    r = fn(g)
+                    if r is not None:
+                        g = r
+                if g is not p.grad:
+                    p.grad.copy_(g)
+            post = getattr(p, "_post_accumulate_grad_hooks", None)
+            if post:
+                for fn in post.values():
+                    fn(p)
 
 
 class ViTFunction(torch.autograd.Function):
@@ -528,6 +652,7 @@ class ViTFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, engine, training, want_probs):
         logits, tape = engine.forward(x, training, save=True, want_probs=want_probs)
+        tape.x_grad = ctx.needs_input_grad[0]
         ctx.engine = engine
         ctx.tape = tape
         return logits
@@ -536,6 +661,7 @@ class ViTFunction(torch.autograd.Function):
     def backward(ctx, dlogits):
         if ctx.tape is None:
             raise RuntimeError("VisionTransformer backward called twice on the same forward")
-        ctx.engine.backward(ctx.tape, dlogits)
+        dimg = ctx.engine.backward(ctx.tape, dlogits)
         ctx.tape = None
-        return None, None, None, None, None
+        ctx.engine.run_param_hooks()
+        return dimg, None, None, None, None

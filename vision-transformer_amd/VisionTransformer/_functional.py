@@ -5,8 +5,9 @@ Every op runs libvit_hip kernels; weights are fp32 masters cast to the activatio
 Gradients flow through standard autograd into each parameter's `.grad`.
 """
 import torch
+import torch.nn.functional as F
 
-from . import _ops
+from . import _cpu, _ops
 from ._ops import ACT_NONE, ACT_RELU
 
 DROPOUT_P = 0.2
@@ -117,8 +118,42 @@ class DropoutFn(torch.autograd.Function):
 def dropout(x, training, p=DROPOUT_P):
     if not training or p == 0.0:
         return x
+    if not x.is_cuda:
+        return F.dropout(x, p, True)                       # host path (_cpu.py)
     seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
     return DropoutFn.apply(x, p, seed)
+
+
+# ---- device dispatch used by the module forwards: ROCm tensors run the HIP ops above, CPU tensors (model and
+# input on the host, train.py --device cpu) run the host path.  A mixed call reaches the HIP op, which raises.
+def _host(*ts):
+    return all(t is None or not t.is_cuda for t in ts)
+
+
+def linear(x, w, b, act):
+    if _host(x, w, b):
+        y = F.linear(x, w, b)
+        return torch.relu(y) if act == ACT_RELU else y
+    return LinearFn.apply(x, w, b, act)
+
+
+def layer_norm(x, g, b):
+    if _host(x, g, b):
+        return F.layer_norm(x, (x.shape[-1],), g, b, 1e-5)
+    return LayerNormFn.apply(x, g, b)
+
+
+def head_attention(x, wq, wk, wv):
+    if _host(x, wq, wk, wv):
+        o, probs = _cpu.attention(x, torch.cat([wq, wk, wv], dim=0), 1, want_probs=True)
+        return o, probs[:, 0].detach()
+    return HeadAttentionFn.apply(x, wq, wk, wv)
+
+
+def patch_embed(x, w, b, cls, pos, P, dtype):
+    if _host(x, w, b, cls, pos):
+        return _cpu.patch_embed(x, w, b, cls, pos, P)
+    return PatchEmbedFn.apply(x, w, b, cls, pos, P, dtype)
 
 
 class HeadAttentionFn(torch.autograd.Function):
@@ -136,8 +171,9 @@ class HeadAttentionFn(torch.autograd.Function):
             _ops.copy2d(w.contiguous(), D, wpack[i * hd:(i + 1) * hd], D, hd, D)
         qkv = _ops.linear(x2, wpack)
         probs = torch.empty(B, 1, T, T, dtype=torch.float32, device=x.device)
-        o, lse = _ops.attn_fwd(qkv, B, T, 1, hd, float(hd) ** 0.5, probs=probs)
-        ctx.save_for_backward(x2, wpack, qkv, o, lse)
+        o32 = torch.empty(B * T, hd, dtype=torch.float32, device=x.device) if dt == torch.bfloat16 else None
+        o, lse = _ops.attn_fwd(qkv, B, T, 1, hd, float(hd) ** 0.5, probs=probs, o32=o32)
+        ctx.save_for_backward(x2, wpack, qkv, o, lse, o32)
         ctx.dims = (B, T, D, hd)
         wei = probs.view(B, T, T)
         ctx.mark_non_differentiable(wei)
@@ -145,10 +181,10 @@ class HeadAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _dwei):
-        x2, wpack, qkv, o, lse = ctx.saved_tensors
+        x2, wpack, qkv, o, lse, o32 = ctx.saved_tensors
         B, T, D, hd = ctx.dims
         d_o = _flat2(dout).to(x2.dtype)
-        dqkv = _ops.attn_bwd(qkv, o, d_o, lse, B, T, 1, hd, float(hd) ** 0.5)
+        dqkv = _ops.attn_bwd(qkv, o, d_o, lse, B, T, 1, hd, float(hd) ** 0.5, o32=o32)
         dx = torch.empty(B * T, D, dtype=x2.dtype, device=x2.device)
         _ops.gemm(dqkv, wpack, dx, B * T, D, 3 * hd, 3 * hd, D, D, b_kcontig=False)
         dw = torch.empty(3 * hd, D, dtype=torch.float32, device=x2.device)

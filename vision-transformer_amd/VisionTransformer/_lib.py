@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
@@ -52,14 +52,15 @@ _SIGS = {
     "vit_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDesc), _P]),
     "vit_gemm_split_k_hint": (ctypes.c_int, [_I64, _I64, _I64, _I32]),
     "vit_im2col": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _I64, _I64, _I64, _I64, _P]),
+    "vit_col2im": (ctypes.c_int, [_P, _I32, _P, _I32, _I64, _I64, _I64, _I64, _I64, _P]),
     "vit_embed_cls": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _I64, _I64, _P]),
     "vit_layernorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64, _F, _I32, _P]),
     "vit_layernorm_bwd_parts": (_I64, [_I64, _I64]),
     "vit_layernorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _F, _U32, _P, _I32, _I64,
                                          _I64, _I32, _P]),
-    "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
+    "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
-    "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _P]),
+    "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _P]),
     "vit_colsum_workspace_bytes": (_I64, [_I64, _I64]),
     "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _P, _P]),
     "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),
@@ -69,6 +70,9 @@ _SIGS = {
     "vit_gelu_fwd": (ctypes.c_int, [_P, _P, _I64, _P]),
     "vit_gelu_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),
     "vit_softmax_xent": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P, _P]),
+    "vit_resize_ksize": (ctypes.c_int, [_I64, _I64]),
+    "vit_resize_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64]),
+    "vit_resize_to_tensor": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _I32, _P, _I64, _P]),
     "vit_adamw": (ctypes.c_int, [_P, _I64, _F, _F, _F, _F, _F, _F, _F, _F, _I32, _P]),
     "vit_pack": (ctypes.c_int, [_P, _I64, _I32, _P]),
 }

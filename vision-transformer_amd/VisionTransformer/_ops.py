@@ -68,6 +68,8 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=
     if need > 0:
         if workspace is None or workspace.numel() * workspace.element_size() < need:
             workspace = torch.empty(need // 4 + 1, dtype=torch.float32, device=c.device)
+            if stream is not None:
+                workspace.record_stream(stream)      # freed on return: not reusable before `stream` is done with it
         d.workspace, d.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
     _lib.check(_lib.load().vit_gemm(ctypes.byref(d), _stream(stream)), "vit_gemm")
     return c
@@ -93,6 +95,14 @@ def im2col(x, P, dtype, stream=None):
     cols = torch.empty(B * n, C * P * P, dtype=dtype, device=x.device)
     _lib.call("vit_im2col", _ptr(x), dtype_code(x), _ptr(cols), dtype_code(dtype), B, C, H, W, P, _stream(stream))
     return cols
+
+
+def col2im(cols, x, P, stream=None):
+    """Inverse of im2col for k = s = P (a permutation): x[B, C, H, W] <- cols[B*N, C*P*P] (input-image gradient)."""
+    _need_cuda(cols, x)
+    B, C, H, W = x.shape
+    _lib.call("vit_col2im", _ptr(cols), dtype_code(cols), _ptr(x), dtype_code(x), B, C, H, W, P, _stream(stream))
+    return x
 
 
 def embed_cls(cls, pos, x0, B, T, D, stream=None):
@@ -129,13 +139,14 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, dr
     return partial
 
 
-def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, stream=None):
+def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, o32=None, stream=None):
+    """o = softmax(scale Q K^T) V per head; `o32` (bf16 only): also store O unrounded (fp32) for attn_bwd's delta."""
     _need_cuda(qkv)
     D = H * hd
     o = torch.empty(B * T, D, dtype=qkv.dtype, device=qkv.device) if o is None else o
     lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device) if lse is None else lse
-    _lib.call("vit_attn_fwd", _ptr(qkv), _ptr(o), _ptr(lse), _ptr(probs), B, T, H, hd, scale, dtype_code(qkv),
-              _stream(stream))
+    _lib.call("vit_attn_fwd", _ptr(qkv), _ptr(o), _ptr(o32), _ptr(lse), _ptr(probs), B, T, H, hd, scale,
+              dtype_code(qkv), _stream(stream))
     return o, lse
 
 
@@ -143,12 +154,12 @@ def attn_bwd_workspace_bytes(B, T, H, hd, dtype):
     return _lib.load().vit_attn_bwd_workspace_bytes(B, T, H, hd, dtype_code(dtype))
 
 
-def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, stream=None):
+def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, o32=None, stream=None):
     dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
     need = attn_bwd_workspace_bytes(B, T, H, hd, qkv.dtype)
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty(max(need // 4, 1), dtype=torch.float32, device=qkv.device)
-    _lib.call("vit_attn_bwd", _ptr(qkv), _ptr(o), _ptr(d_o), _ptr(lse), _ptr(dqkv), B, T, H, hd, scale,
+    _lib.call("vit_attn_bwd", _ptr(qkv), _ptr(o), _ptr(o32), _ptr(d_o), _ptr(lse), _ptr(dqkv), B, T, H, hd, scale,
               dtype_code(qkv), _ptr(workspace), _stream(stream))
     return dqkv
 

@@ -3,7 +3,8 @@
 Constructor signatures, sub-module names and parameter registration order are those of the reference, so
 `state_dict()` keys, shapes and the random-init draw order are identical (verified bit-for-bit against the
 reference in tests/test_dropin_cpu.py).  The arithmetic is not torch's: every forward here runs libvit_hip kernels
-(module-level path, `_functional.py`).  `VisionTransformer.forward` does not call these forwards at all — it runs
+(module-level path, `_functional.py`) on ROCm tensors; on CPU tensors they run the host path (`_cpu.py`,
+train.py --device cpu).  `VisionTransformer.forward` does not call these forwards at all — it runs
 the fused whole-model engine (`_engine.py`) over the same parameters.
 
 Reference semantics kept:
@@ -31,7 +32,7 @@ class Head(nn.Module):
         self.block_size = block_size
 
     def forward(self, x):
-        return Fh.HeadAttentionFn.apply(x, self.query.weight, self.key.weight, self.value.weight)
+        return Fh.head_attention(x, self.query.weight, self.key.weight, self.value.weight)
 
 
 class MultiHeadAttention(nn.Module):
@@ -45,7 +46,7 @@ class MultiHeadAttention(nn.Module):
     def forward(self, x):
         pairs = [head(x) for head in self.heads]
         out = torch.cat([o for o, _ in pairs], dim=-1)
-        out = Fh.LinearFn.apply(out, self.proj.weight, self.proj.bias, ACT_NONE)
+        out = Fh.linear(out, self.proj.weight, self.proj.bias, ACT_NONE)
         out = Fh.dropout(out, self.training, self.dropout.p)
         self.attention_probs = torch.stack([w for _, w in pairs], dim=1)
         return out
@@ -59,8 +60,8 @@ class FeedForward(nn.Module):
 
     def forward(self, x):
         fc1, _, fc2, drop = self.mlp
-        h = Fh.LinearFn.apply(x, fc1.weight, fc1.bias, ACT_RELU)          # ReLU fused in the GEMM epilogue
-        y = Fh.LinearFn.apply(h, fc2.weight, fc2.bias, ACT_NONE)
+        h = Fh.linear(x, fc1.weight, fc1.bias, ACT_RELU)          # ReLU fused in the GEMM epilogue
+        y = Fh.linear(h, fc2.weight, fc2.bias, ACT_NONE)
         return Fh.dropout(y, self.training, drop.p)
 
 
@@ -74,8 +75,8 @@ class Block(nn.Module):
         self.ln2 = nn.LayerNorm(n_embd)
 
     def forward(self, x):
-        x = x + self.multi_head(Fh.LayerNormFn.apply(x, self.ln1.weight, self.ln1.bias))
-        x = x + self.ffwd(Fh.LayerNormFn.apply(x, self.ln2.weight, self.ln2.bias))
+        x = x + self.multi_head(Fh.layer_norm(x, self.ln1.weight, self.ln1.bias))
+        x = x + self.ffwd(Fh.layer_norm(x, self.ln2.weight, self.ln2.bias))
         return x
 
 

@@ -10,13 +10,26 @@ Extra (additive) API:
   * `model.store_attention_probs = True` — fill each block's `multi_head.attention_probs` [B, H, T, T] during the
     fused forward (the reference always materialises it, transformer.py:48; here it is opt-in because it is 477 MB
     per layer at ViT-B/16, B=256);
-  * `model.enable_data_parallel(group=None)` — all-reduce (average) gradients over `torch.distributed` (RCCL)
-    bucket-by-bucket while the backward is still running;
-  * `model.hip_engine` — the engine (flat gradient / shadow-weight buffers).
+  * `model.enable_data_parallel(group=None, force=False)` — all-reduce (average) gradients over `torch.distributed`
+    (RCCL) bucket-by-bucket while the backward is still running.  Use this instead of wrapping the model in
+    `torch.nn.parallel.DistributedDataParallel` (which is detected and refused: the fused engine is one autograd
+    node, so DDP's per-parameter reducer hooks would never fire);
+  * `model.hip_engine` — the engine (flat gradient / shadow-weight buffers).  After writing the fp32 parameters
+    out-of-band (through `p.data`, which autograd does not version), call `model.hip_engine.repack()`;
+    `load_state_dict` and in-place writes on the parameters themselves are detected automatically.
+
+Device semantics (the reference picks 'cuda' or 'cpu', train.py:26): a model on a ROCm device runs the fused HIP
+engine and fails loudly when libvit_hip.so is missing; a model on the CPU runs the host path `_cpu.py` (plain torch
+ops, standard autograd).  A CUDA input never falls back to the host path.
+
+Gradient semantics kept from the reference module: `requires_grad=False` parameters get no gradient (`.grad` stays
+None and their weight-gradient GEMMs are skipped), `x.requires_grad` yields the input gradient, and parameter hooks
+(`register_hook`, `register_post_accumulate_grad_hook`) run once per backward, after the gradients are complete.
 """
 import torch
 import torch.nn as nn
 
+from . import _cpu
 from . import _functional as Fh
 from . import config as _config  # noqa: F401  (reference module imports config alongside transformer)
 from . import transformer
@@ -41,8 +54,8 @@ class PatchEmbedding(nn.Module):
 
     def forward(self, x):
         conv = self.sequence[0]
-        return Fh.PatchEmbedFn.apply(x, conv.weight, conv.bias, self.cls_tkn_embd, self.pos_embd, self.patch_size,
-                                     self.compute_dtype)
+        return Fh.patch_embed(x, conv.weight, conv.bias, self.cls_tkn_embd, self.pos_embd, self.patch_size,
+                              self.compute_dtype)
 
 
 class VisionTransformer(nn.Module):
@@ -82,19 +95,49 @@ class VisionTransformer(nn.Module):
             self._engine = Engine(self)
         return self._engine
 
-    def enable_data_parallel(self, group=None):
-        """Average gradients across the process group with RCCL, bucketed per block, overlapped with backward."""
+    def enable_data_parallel(self, group=None, force=False):
+        """Average gradients across the process group with RCCL, bucketed per block, overlapped with backward.
+        `force` keeps the all-reduce path on even for a world of one rank (tests the collective on one GPU)."""
         import torch.distributed as dist
         if not dist.is_initialized():
             raise RuntimeError("enable_data_parallel: torch.distributed is not initialised")
         eng = self.hip_engine
         eng.ddp_group = group
-        eng.ddp_enabled = dist.get_world_size(group) > 1
+        eng.ddp_enabled = bool(force) or dist.get_world_size(group) > 1
         return self
 
+    # the engine holds a weakref to its model and views of the parameters: never copy or pickle it (a deep copy or
+    # an unpickled model builds its own engine on first use)
+    def __getstate__(self):
+        state = dict(super().__getstate__())
+        state["_engine"] = None
+        state["_anchor"] = None
+        return state
+
+    def __deepcopy__(self, memo):
+        import copy
+        cls = self.__class__
+        new = cls.__new__(cls)
+        memo[id(self)] = new
+        for k, v in self.__getstate__().items():
+            object.__setattr__(new, k, copy.deepcopy(v, memo))
+        return new
+
+    def _check_not_ddp_wrapped(self):
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        active = DDP._get_active_ddp_module()
+        if active is not None and any(m is self for m in active.module.modules()):
+            raise RuntimeError(
+                "VisionTransformer must not be wrapped in torch.nn.parallel.DistributedDataParallel: the fused HIP "
+                "engine is a single autograd node, so DDP's per-parameter reducer would never see the gradients. "
+                "Call model.enable_data_parallel() instead (bucketed RCCL all-reduce overlapped with the backward).")
+
     def forward(self, x):
+        if not x.is_cuda and all(not p.is_cuda for p in (self.mlp[3].weight, self.emdeddings.pos_embd)):
+            return _cpu.vit_forward(self, x)              # host path: the model lives on the CPU (train.py:26)
+        self._check_not_ddp_wrapped()
         eng = self.hip_engine
-        want_grad = torch.is_grad_enabled() and any(p.requires_grad for p in (self.mlp[3].weight,))
+        want_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
         if want_grad:
             if self._anchor is None or self._anchor.device != x.device:
                 self._anchor = torch.zeros((), device=x.device, requires_grad=True)

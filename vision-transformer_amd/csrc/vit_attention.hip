@@ -30,7 +30,8 @@ constexpr int GA_HDMAX = 128;
 template <class T>
 __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ qkv, T* __restrict__ o,
                                                         float* __restrict__ lse, float* __restrict__ probs, int64_t B,
-                                                        int64_t Tn, int64_t H, int64_t hd, float scale) {
+                                                        int64_t Tn, int64_t H, int64_t hd, float scale,
+                                                        float* __restrict__ o32 = nullptr) {
   __shared__ float sc[4][GA_TMAX];
   __shared__ float qs[4][GA_HDMAX];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ qk
     float acc = 0.f;
     for (int64_t j = 0; j < Tn; ++j) acc += sc[w][j] * ld1<T>(base + j * ld + 2 * D + h * hd + d);
     if (valid) st1<T>(o + (b * Tn + q) * D + h * hd + d, acc);
+    if (valid && o32) o32[(b * Tn + q) * D + h * hd + d] = acc;
   }
   if (lane == 0 && valid) lse[bh * Tn + q] = mx + logf(l);
 }
@@ -80,7 +82,8 @@ __global__ __launch_bounds__(256) void attn_bwd_generic_rows(const T* __restrict
                                                              const T* __restrict__ d_o, const float* __restrict__ lse,
                                                              T* __restrict__ dqkv, float* __restrict__ Pws,
                                                              float* __restrict__ dSws, int64_t B, int64_t Tn,
-                                                             int64_t H, int64_t hd, float scale) {
+                                                             int64_t H, int64_t hd, float scale,
+                                                             const float* __restrict__ o32 = nullptr) {
   __shared__ float ds_s[4][GA_TMAX];
   __shared__ float qs[4][GA_HDMAX];
   __shared__ float dos[4][GA_HDMAX];
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(256) void attn_bwd_generic_rows(const T* __restrict
     qs[w][d] = ld1<T>(base + q * ld + h * hd + d);
     const float g = ld1<T>(d_o + (b * Tn + q) * D + h * hd + d);
     dos[w][d] = g;
-    dl += g * ld1<T>(o + (b * Tn + q) * D + h * hd + d);
+    dl += g * (o32 ? o32[(b * Tn + q) * D + h * hd + d] : ld1<T>(o + (b * Tn + q) * D + h * hd + d));
   }
   dl = wave_sum(dl);
   __syncthreads();
@@ -235,7 +238,8 @@ VIT_DEV f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 VIT_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
-                                                     float* __restrict__ lse, int64_t Tn, int64_t H, float scale) {
+                                                     float* __restrict__ o32, float* __restrict__ lse, int64_t Tn,
+                                                     int64_t H, float scale) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];  // [buf][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
   const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
@@ -320,6 +324,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
         float v[4] = {oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv, oacc[db][4 * g + 2] * inv,
                       oacc[db][4 * g + 3] * inv};
         st4<bf16_t>(orow + db * 32 + 8 * g + 4 * hf, v);
+        if (o32) st4<float>(o32 + (b * Tn + q) * D + h * HD + db * 32 + 8 * g + 4 * hf, v);
       }
     }
     if (hf == 0) lse[bh * Tn + q] = (m_run + log2f(l_tot)) / LOG2E;
@@ -329,7 +334,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
 // delta[b,h,q] = sum_d dO . O  (fp32): 8 lanes per (row, head), one 16-B chunk each, so a wave instruction reads 8
 // whole 128-B head rows; fixed shuffle-tree order.  (One thread per (row, head) read 64 lines per instruction: 6x
 // off the HBM rate at T = 577.)
-__global__ __launch_bounds__(256) void attn_delta(const bf16_t* __restrict__ o, const bf16_t* __restrict__ d_o,
+// With the forward's fp32 O (o32) delta is exact to fp32: under the reference's x sqrt(hd) scaling most softmax rows are
+// saturated, where dS = P (dP - delta) is a tiny difference and delta from the bf16-rounded O swamps it (measured: the
+// Q / K weight gradients of a saturated head 10x off the bf16-rounding oracle).
+template <class TO>
+__global__ __launch_bounds__(256) void attn_delta(const TO* __restrict__ o, const bf16_t* __restrict__ d_o,
                                                   float* __restrict__ delta, int64_t B, int64_t Tn, int64_t H) {
   const int64_t total = B * Tn * H * 8;               // a multiple of 8: the 8 lanes of a row leave the loop together
   const int64_t D = H * HD;
@@ -337,11 +346,13 @@ __global__ __launch_bounds__(256) void attn_delta(const bf16_t* __restrict__ o, 
     const int64_t u = t >> 3;
     const int c = (int)(t & 7);
     const int64_t row = u / H, h = u % H, b = row / Tn, q = row % Tn;
-    const s16x8 va = *reinterpret_cast<const s16x8*>(o + row * D + h * HD + c * 8);
     const s16x8 vg = *reinterpret_cast<const s16x8*>(d_o + row * D + h * HD + c * 8);
+    float va[8];
+    ld4<TO>(o + row * D + h * HD + c * 8, va);
+    ld4<TO>(o + row * D + h * HD + c * 8 + 4, va + 4);
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += bf2f((bf16_t)va[j]) * bf2f((bf16_t)vg[j]);
+    for (int j = 0; j < 8; ++j) s += va[j] * bf2f((bf16_t)vg[j]);
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
@@ -645,8 +656,8 @@ VIT_DEV void dma_slice_g(const bf16_t* base, int64_t row0, int64_t ld, int64_t c
 template <int NQB>
 __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                          const bf16_t* __restrict__ d_o, const float* __restrict__ lse,
-                                                         bf16_t* __restrict__ dqkv, int64_t Tn64, int64_t H,
-                                                         int64_t items, float scale) {
+                                                         const float* __restrict__ delta_in, bf16_t* __restrict__ dqkv,
+                                                         int64_t Tn64, int64_t H, int64_t items, float scale) {
   constexpr int Tp = NQB * 32;                        // T rounded up to 32 (compile time: the dQ sum unrolls)
   constexpr int nqb = NQB;
   constexpr int IMG = Tp * HD;                        // elements per [Tp][64] image
@@ -717,10 +728,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(base + o));
   };
 
-  // lse of item `it_` -> a register (tid < Tn <= 256)
-  float lreg = 0.f;
+  // lse (and delta, when precomputed from the fp32 O) of item `it_` -> registers (tid < Tn <= 256)
+  const bool dglob = delta_in != nullptr;
+  float lreg = 0.f, dreg = 0.f;
   auto load_lse = [&](int64_t it_) {
-    if (tid < Tn) lreg = lse[it_ * Tn + tid];
+    if (tid < Tn) {
+      lreg = lse[it_ * Tn + tid];
+      if (dglob) dreg = delta_in[it_ * Tn + tid];
+    }
   };
 
   int64_t item = blockIdx.x;
@@ -729,7 +744,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     dma_slice_g(qkv, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane);
     dma_slice_g(qkv, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
     dma_slice_g(d_o, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
-    dma_slice_g(o, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);   // O: only needed for delta
+    if (!dglob) dma_slice_g(o, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);   // O: only needed for delta
     if (VLDS) dma_slice_g(qkv, b * Tn, ld, 2 * D + h * HD, Tn, Tp, Vs, wave, lane);
     load_lse(item);
   }
@@ -741,9 +756,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     const int64_t nb_ = more ? nxt / H : 0, nh_ = more ? nxt % H : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / O DMA, lse
     if (tid < Tp) lse2s[tid] = tid < Tn ? lreg * LOG2E : INFINITY;
+    if (dglob && tid < Tp) dlts[tid] = tid < Tn ? dreg : 0.f;
     __syncthreads();                                  // every wave's DMA landed
     // delta[q] = sum_d dO[q][d] O[q][d]: 8 lanes per row (one 16-B chunk each), fixed shuffle-tree order
-    for (int q = tid; q < Tp * 8; q += 512) {         // Tp * 8 is a multiple of 256: wave-uniform condition
+    for (int q = tid; q < (dglob ? 0 : Tp * 8); q += 512) {   // Tp * 8 is a multiple of 256: wave-uniform condition
       {
         const int r = q >> 3, c = q & 7;
         const int off = r * HD + ((c ^ aswz(r)) << 3);
@@ -881,13 +897,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     lds_barrier();                                    // images read before the next item's DMA overwrites them
     if (more) {
       dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
-      dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
+      if (!dglob) dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
     }
 #else
     // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K and O
     if (more) {
       dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
-      dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
+      if (!dglob) dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
     }
     if (kact && key < Tn) {
       bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD;
@@ -920,8 +936,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 // ---------------------------------------------------------------------------------------------------------------
 template <int NKB>
 __global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
-                                                           float* __restrict__ lse, int64_t Tn64, int64_t H,
-                                                           float scale) {
+                                                           float* __restrict__ o32, float* __restrict__ lse,
+                                                           int64_t Tn64, int64_t H, float scale) {
   constexpr int Tp = NKB * 32;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * Tp * HD];
   bf16_t* Ks = smem;
@@ -982,6 +998,17 @@ __global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restr
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = 1.0f / l_tot;
   const int q = q0 + (lane & 31);
+  if (o32 && q < Tn) {                               // fp32 O for the backward's delta (training forward only)
+    float* orow32 = o32 + (b * Tn + q) * D + h * HD + 4 * hf;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float v[4] = {oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv, oacc[db][4 * g + 2] * inv,
+                            oacc[db][4 * g + 3] * inv};
+        st4<float>(orow32 + db * 32 + 8 * g, v);
+      }
+  }
   // lane (q, hf) holds O[q][8k + 4hf .. 8k + 4hf + 3] in group k = 4db + g; one permlane32 swap per dword pairs groups
   // (k, k+1) into 16 contiguous bytes per lane: columns 8k..8k+7 on lanes < 32, 8k+8..8k+15 on lanes >= 32
   uint32_t pk[8][2];
@@ -1011,14 +1038,15 @@ bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD;
 
 }  // namespace
 
-extern "C" int vit_attn_fwd(const void* qkv, void* o, float* lse, float* probs, int64_t B, int64_t T, int64_t H,
-                            int64_t hd, float scale, int32_t dtype, void* stream) {
+extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, float* probs, int64_t B, int64_t T,
+                            int64_t H, int64_t hd, float scale, int32_t dtype, void* stream) {
   VIT_REQUIRE(qkv && o && lse && B > 0 && T > 0 && H > 0 && hd > 0, "vit_attn_fwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && probs == nullptr) {
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
     if (T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_FWD_SPLIT")) {
-#define FWD(NK) attn_fwd_fused<NK><<<(unsigned)(B * H), NK * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, scale)
+#define FWD(NK) \
+  attn_fwd_fused<NK><<<(unsigned)(B * H), NK * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, scale)
       switch ((int)((T + 31) / 32)) {
         case 1: FWD(1); break;
         case 2: FWD(2); break;
@@ -1032,12 +1060,15 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* lse, float* probs, 
 #undef FWD
     } else {
       dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
-      attn_fwd_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, scale);
+      attn_fwd_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, scale);
     }
   } else {
     VIT_REQUIRE(T <= GA_TMAX && hd <= GA_HDMAX, "vit_attn_fwd(generic): T<=%d, hd<=%d", GA_TMAX, GA_HDMAX);
+    VIT_REQUIRE(o32 == nullptr || dtype == VIT_BF16, "vit_attn_fwd: o32 is for bf16 outputs only");
     dim3 grid((unsigned)((T + 3) / 4), (unsigned)(B * H));
-    if (dtype == VIT_BF16)
+    if (dtype == VIT_BF16 && o32)
+      attn_fwd_generic<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, probs, B, T, H, hd, scale, o32);
+    else if (dtype == VIT_BF16)
       attn_fwd_generic<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, probs, B, T, H, hd, scale);
     else
       attn_fwd_generic<float><<<grid, 256, 0, s>>>((const float*)qkv, (float*)o, lse, probs, B, T, H, hd, scale);
@@ -1050,20 +1081,27 @@ extern "C" int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H,
   return 2 * B * H * T * T * (int64_t)sizeof(float);
 }
 
-extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, const float* lse, void* dqkv, int64_t B,
-                            int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace,
-                            void* stream) {
+extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d_o, const float* lse,
+                            void* dqkv, int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype,
+                            void* workspace, void* stream) {
   VIT_REQUIRE(qkv && o && d_o && lse && dqkv && workspace && B > 0 && T > 0 && H > 0 && hd > 0,
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
+  const int64_t rows = B * T * H;
+  const unsigned dgrid = (unsigned)std::min<int64_t>((rows * 8 + 255) / 256, 16384);
   if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_BWD_SPLIT")) {
     // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid
     const int64_t items = B * H;
+    const float* dl = nullptr;             // without o32 the kernel computes delta from the bf16 O itself
+    if (o32) {
+      attn_delta<float><<<dgrid, 256, 0, s>>>(o32, (const bf16_t*)d_o, (float*)workspace, B, T, H);
+      dl = (const float*)workspace;
+    }
     int64_t grid = std::min<int64_t>(items, vit_cu_count());
     if (const char* e = getenv("VIT_ATTN_BWD_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(items, atoll(e)));
 #define BWD(NQ)                                                                                                  \
   attn_bwd_fused<NQ><<<(unsigned)grid, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \
-                                                    (bf16_t*)dqkv, T, H, items, scale)
+                                                    dl, (bf16_t*)dqkv, T, H, items, scale)
     switch ((int)((T + 31) / 32)) {
       case 1: BWD(1); break;
       case 2: BWD(2); break;
@@ -1077,9 +1115,8 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, con
 #undef BWD
   } else if (use_mfma(dtype, hd)) {
     float* delta = (float*)workspace;
-    const int64_t rows = B * T * H;
-    attn_delta<<<(unsigned)std::min<int64_t>((rows * 8 + 255) / 256, 16384), 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)d_o,
-                                                                                 delta, B, T, H);
+    if (o32) attn_delta<float><<<dgrid, 256, 0, s>>>(o32, (const bf16_t*)d_o, delta, B, T, H);
+    else attn_delta<bf16_t><<<dgrid, 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)d_o, delta, B, T, H);
     dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
     attn_bwd_dq_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
                                           scale);
@@ -1092,7 +1129,7 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const void* d_o, con
     dim3 grid((unsigned)((T + 3) / 4), (unsigned)(B * H));
     if (dtype == VIT_BF16) {
       attn_bwd_generic_rows<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse,
-                                                         (bf16_t*)dqkv, Pws, dSws, B, T, H, hd, scale);
+                                                         (bf16_t*)dqkv, Pws, dSws, B, T, H, hd, scale, o32);
       attn_bwd_generic_cols<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, (bf16_t*)dqkv, Pws,
                                                          dSws, B, T, H, hd, scale);
     } else {

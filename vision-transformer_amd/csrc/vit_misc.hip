@@ -55,6 +55,18 @@ __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ x, T
   }
 }
 
+// col2im for k = s = P: one thread per image element (b, c, h, w), coalesced on the image write.
+template <class TI, class TO>
+__global__ __launch_bounds__(256) void col2im_kernel(const TI* __restrict__ cols, TO* __restrict__ x, int64_t B,
+                                                     int64_t C, int64_t H, int64_t W, int64_t P) {
+  const int64_t nw = W / P, N = (H / P) * nw, KC = C * P * P, total = B * C * H * W;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = t % W, h = (t / W) % H, c = (t / (W * H)) % C, b = t / (W * H * C);
+    const int64_t n = (h / P) * nw + w / P, col = (c * P + h % P) * P + w % P;
+    st1<TO>(x + t, ld1<TI>(cols + (b * N + n) * KC + col));
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void embed_cls_kernel(const float* __restrict__ cls, const float* __restrict__ pos,
                                                         T* __restrict__ x0, int64_t B, int64_t T_, int64_t D) {
@@ -295,6 +307,26 @@ extern "C" int vit_im2col(const void* x, int32_t x_dtype, void* cols, int32_t dt
     return VIT_ERR_INVALID;
   }
   return vit::check_launch("vit_im2col");
+}
+
+extern "C" int vit_col2im(const void* cols, int32_t dtype, void* x, int32_t x_dtype, int64_t B, int64_t C,
+                          int64_t H, int64_t W, int64_t P, void* stream) {
+  VIT_REQUIRE(x && cols, "vit_col2im: null pointer");
+  VIT_REQUIRE(B > 0 && C > 0 && P > 0 && H % P == 0 && W % P == 0, "vit_col2im: image %lldx%lld not divisible by P=%lld",
+              (long long)H, (long long)W, (long long)P);
+  const unsigned grid = grid_for(B * C * H * W, 256, 16384);
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16 && x_dtype == VIT_F32)
+    col2im_kernel<bf16_t, float><<<grid, 256, 0, s>>>((const bf16_t*)cols, (float*)x, B, C, H, W, P);
+  else if (dtype == VIT_F32 && x_dtype == VIT_F32)
+    col2im_kernel<float, float><<<grid, 256, 0, s>>>((const float*)cols, (float*)x, B, C, H, W, P);
+  else if (dtype == VIT_BF16 && x_dtype == VIT_BF16)
+    col2im_kernel<bf16_t, bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)cols, (bf16_t*)x, B, C, H, W, P);
+  else {
+    vit::set_error("vit_col2im: unsupported dtype pair %d->%d", dtype, x_dtype);
+    return VIT_ERR_INVALID;
+  }
+  return vit::check_launch("vit_col2im");
 }
 
 extern "C" int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, int64_t B, int64_t T,

@@ -7,6 +7,9 @@ loss, step} (:107-113), so checkpoints interchange with the reference (per-head 
 keys).  The hot loop (:89-102) runs on the MI355X path: fused HIP forward/backward, fused softmax cross-entropy,
 FusedAdamW (one multi-tensor launch), and — under torchrun — gradient all-reduce over RCCL overlapped with the
 backward.  The per-step `loss.item()` host sync of the reference is kept only when logging asks for it.
+Without a GPU (or with `--device cpu`) the same loop runs the package's host path (VisionTransformer/_cpu.py, plain
+torch ops on all host cores, torch.optim.AdamW) — the reference's own behaviour (train.py:26,80) and BASELINE config 1
+(ViT-Tiny/16 64^2 B8 fp32, `python train.py --device cpu`).
 
 Differences (documented in DESIGN.md): hyper-parameters come from flags instead of hard-coded constants (the
 reference's TODO at :124-125); data defaults to a synthetic CIFAR-shaped stream because the container has no network
@@ -24,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from VisionTransformer import config, vit
-from VisionTransformer.optim import FusedAdamW, cross_entropy
+from VisionTransformer.optim import cross_entropy, make_optimizer
 
 device = "cuda" if torch.cuda.is_available() else "cpu"
 
@@ -105,21 +108,25 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
     saved_epoch = search_checkpoint(checkpoint_dir)
     torch.manual_seed(0)                              # identical init on every rank
     model = vit.VisionTransformer(configs)
-    optimizer = FusedAdamW(model.parameters(), lr=lr, weight_decay=1e-4)
+    optimizer = make_optimizer(model.parameters(), lr=lr, weight_decay=1e-4, device=device)
     iteration = 0
     if saved_epoch is not None:
         print(f"Checkpoint Found. Loading model from epoch {saved_epoch}")
         ckpt = torch.load(os.path.join(checkpoint_dir, f"{saved_epoch}.pt"), map_location="cpu", weights_only=True)
         model.load_state_dict(ckpt["model_state_dict"])
         model = model.to(device)
-        optimizer = FusedAdamW(model.parameters(), lr=lr, weight_decay=1e-4)
+        optimizer = make_optimizer(model.parameters(), lr=lr, weight_decay=1e-4, device=device)
         optimizer.load_state_dict(ckpt["optimizer_state_dict"])
         iteration = int(ckpt.get("step", 0))
     else:
         saved_epoch = 0
         model = model.to(device)
+    net = model
     if world > 1:
-        model.enable_data_parallel()
+        if device == "cpu":      # host path: standard autograd, so torch's own DDP (gloo) applies
+            net = torch.nn.parallel.DistributedDataParallel(model)
+        else:
+            model.enable_data_parallel()
     writer = _writer(log_dir) if rank == 0 else None
     running_loss = 0.0
     for epoch in range(saved_epoch, epochs + 1):
@@ -129,7 +136,7 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
         for tensors, labels in train_loader:
             tensors = tensors.to(device, non_blocking=True)
             labels = labels.to(device, non_blocking=True)
-            logits = model(tensors)
+            logits = net(tensors)
             loss = cross_entropy(logits, labels)
             optimizer.zero_grad(set_to_none=True)
             loss.backward()
@@ -160,6 +167,33 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
     return running_loss
 
 
+def time_steps(configs, steps, warmup, lr=1e-4, dev=None, seed=1234):
+    """The hot loop body (train.py:91-98: forward, CE loss, zero_grad(set_to_none), backward, AdamW step) on one
+    synthetic batch already resident on `dev`, dropout on; returns (seconds per timed step, last loss).  This is the
+    repo's own CPU training step that bench.py's `cpu_baseline` times (BASELINE config 1)."""
+    dev = torch.device(dev or device)
+    torch.manual_seed(0)
+    model = vit.VisionTransformer(configs).to(dev).train()
+    opt = make_optimizer(model.parameters(), lr=lr, weight_decay=1e-4, device=dev)
+    g = torch.Generator().manual_seed(seed)
+    n_img = int(round((configs.num_patches ** 0.5) * configs.patch_size))
+    x = torch.randn(configs.batch_size, configs.input_channels, n_img, n_img, generator=g).to(dev)
+    y = torch.randint(0, configs.num_classes, (configs.batch_size,), generator=g).to(dev)
+    loss = None
+    t0 = time.perf_counter()
+    for i in range(warmup + steps):
+        if i == warmup:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+        loss = cross_entropy(model(x), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    last = float(loss.item())
+    return (time.perf_counter() - t0) / max(steps, 1), last
+
+
 def main():
     ap = argparse.ArgumentParser(description="ViT training on MI355X (drop-in for the reference src/train.py)")
     ap.add_argument("--model", default="tiny", choices=sorted(config.PRESETS))
@@ -178,15 +212,26 @@ def main():
     ap.add_argument("--checkpoint-dir", default="../checkpoints")
     ap.add_argument("--log-dir", default="../logs")
     ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="auto = cuda when a ROCm GPU is present, else cpu (train.py:26)")
+    ap.add_argument("--threads", type=int, default=0, help="host-path threads (0 = every core this process may use)")
+    ap.add_argument("--bench", action="store_true",
+                    help="time --steps steps (after --warmup) on one resident synthetic batch; print one JSON line")
+    ap.add_argument("--warmup", type=int, default=5)
     args = ap.parse_args()
-    if device != "cuda":
-        raise SystemExit("train.py runs the MI355X HIP path and needs a ROCm GPU (the CPU restatement lives in "
-                         "oracle/ as test infrastructure)")
+    global device
+    if args.device != "auto":
+        device = args.device
+    if device == "cpu":
+        torch.set_num_threads(args.threads or len(os.sched_getaffinity(0)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if device == "cuda":
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     rank, world = _rank_world()
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     n_patches = (args.img // args.patch) ** 2
@@ -194,6 +239,14 @@ def main():
     cfg = config.ViTConfig(input_channels=3, num_classes=args.classes, num_patches=n_patches, embedding_size=D,
                            patch_size=args.patch, num_heads=H, num_blocks=L, precision=dtype,
                            batch_size=args.batch, device="cpu")
+    if args.bench:
+        steps = args.steps or 30
+        sec, last = time_steps(cfg, steps, args.warmup, lr=args.lr)
+        print(json.dumps({"device": device, "model": args.model, "img": args.img, "batch": args.batch,
+                          "dtype": args.dtype, "threads": torch.get_num_threads(), "warmup": args.warmup,
+                          "steps": steps, "ms_per_step": round(sec * 1e3, 3),
+                          "images_per_s": round(args.batch / sec, 3), "final_loss": round(last, 5)}), flush=True)
+        return
     if args.cifar_root:
         import torchvision.transforms as transforms
         from torchvision.datasets import CIFAR10
@@ -204,11 +257,12 @@ def main():
         train_set = SyntheticImages(args.train_size, 3, args.img, args.classes, seed=1 + rank)
         test_set = SyntheticImages(args.test_size, 3, args.img, args.classes, seed=10_000)
     sampler = torch.utils.data.DistributedSampler(train_set) if world > 1 else None
+    pin = device == "cuda"
     train_loader = torch.utils.data.DataLoader(train_set, batch_size=args.batch, shuffle=sampler is None,
                                                sampler=sampler, num_workers=args.workers, drop_last=True,
-                                               pin_memory=True)
+                                               pin_memory=pin)
     test_loader = torch.utils.data.DataLoader(test_set, batch_size=args.batch, num_workers=args.workers,
-                                              drop_last=True, pin_memory=True)
+                                              drop_last=True, pin_memory=pin)
     train(cfg, train_loader, test_loader, args.epochs, args.eval_iter, args.log_dir, args.checkpoint_dir,
           lr=args.lr, max_steps=args.steps)
     if world > 1:
