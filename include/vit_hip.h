@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 4
+#define VIT_ABI_VERSION 5
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1 } vit_dtype;
@@ -103,10 +103,12 @@ int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, i
  *   fwd: y = (x - mean) * rstd * gamma + beta; saves mean/rstd [rows].
  *   bwd: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
  *        dx_out = dx (+ dres when dres != NULL)                    — fused residual-gradient add (transformer.py:77-78)
- *        drop_out = dx_out * keep(drop_seed, i*cols + j) / (1-p)    — fused dropout backward of the producer branch
+ *        drop_out = dx_out * keep(drop_seed, i*cols + j)            — fused dropout backward of the producer branch,
+ *                   WITHOUT the 1/(1-p) scale (exact in bf16: the consumers apply it, e.g. as GEMM alpha)
  *        dgamma/dbeta: per-workgroup partials in `partial` [2][nparts][cols], reduced by vit_colsum_finish
  *        (deterministic); with `osum` != 0 also partial [2] = column sums of the stored gradient output (drop_out
- *        when given, else dx_out) — the bias gradient of the Linear that consumes it, so [3][nparts][cols].
+ *        / (1-p) when drop_out is given, else dx_out) — the bias gradient of the Linear that consumes it, so
+ *        [3][nparts][cols].
  * ------------------------------------------------------------------------------------------------------------ */
 int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma, const float* beta, void* y, int64_t ldy,
                       float* mean, float* rstd, int64_t rows, int64_t cols, float eps, int32_t dtype, void* stream);
@@ -138,25 +140,27 @@ int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d
 
 /* ------------------------------------------------------------------------------------------------------------
  * Reductions / elementwise.
- *   vit_colsum: out[j] = beta*out[j] + sum_i x[i*ldx + j]  (bias / pos / LN-affine gradients); deterministic.
+ *   vit_colsum: out[j] = beta*out[j] + alpha * sum_i x[i*ldx + j]  (bias / pos / LN-affine gradients); deterministic.
  *   vit_colsum_finish: outs[s][j] = beta*outs[s][j] + sum_p part[s][p][j] for s < nsets (<= 3), summed in a fixed
  *               order — second stage of the column sums fused into vit_gemm (colsum_part) / vit_layernorm_bwd.
  *   vit_copy2d: dst[orow(i)*ldd + j] = beta*dst + src[irow(i)*lds + j] with optional row grouping on the source
  *               (irow(i) = (i/G)*Gs + i%G) — token-0 gather (vit.py:80), CLS-gradient copy, dropout-free casts.
- *   vit_dropout_bwd: y = x * keep(seed, i) / (1-p)  (transformer.py:47,59 backward).
+ *   vit_dropout_bwd: y = x * keep(seed, i) * scale  (transformer.py:47,59 backward: scale = 1/(1-p); the engine
+ *                    passes 1 and folds 1/(1-p) into the consumers, so the stored masked gradient is exact).
  *   vit_gelu_fwd/bwd: exact-erf GELU (vit.py:71) on f32.
  *   vit_softmax_xent: per-row softmax cross entropy (train.py:81,93): loss = mean_i(-log p[i][y_i]) and
  *                     dlogits = (softmax - onehot) / rows, in one pass.
  * ------------------------------------------------------------------------------------------------------------ */
 int64_t vit_colsum_workspace_bytes(int64_t rows, int64_t cols);
-int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t cols, float* out, float beta,
-               void* workspace, void* stream);
+int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t cols, float* out, float alpha,
+               float beta, void* workspace, void* stream);
 int vit_colsum_finish(const float* part, int64_t nparts, int64_t cols, int32_t nsets, float* out0, float* out1,
                       float* out2, float beta, void* stream);
 int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,
                int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
                void* stream);
-int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed, void* stream);
+int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed, float scale,
+                    void* stream);
 /* dx = dy * (y > 0): ReLU backward for the module-level FeedForward path (transformer.py:57). */
 int vit_relu_bwd(const void* dy, const void* y, void* dx, int32_t dtype, int64_t n, void* stream);
 int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream);

@@ -54,13 +54,18 @@ def _hd64_cfg(img=64, batch=3, blocks=2):
 @pytest.mark.parametrize("train", [False, True])
 def test_base_width_bf16_engine_vs_oracle(train):
     """C2 shapes through the engine in bf16: D=768, H=12 (hd 64), T=197 (224^2 / 16), L=2, B=2, nc=1000.
-    Gate: logits within 1e-2 (norm-wise) of the bf16-rounding oracle; every gradient's error vs the
-    fp32 oracle at most max(3e-2, 2x) the error of a valid bf16 evaluation, and the whole gradient vector at most 2x.
-    "Valid bf16 evaluation" = the oracle rounding to bf16 at the same storage points, with fp32 or with fp64
-    arithmetic between them: under the saturating x sqrt(hd) softmax the two already differ by up to ~21% on single
-    query / key weight gradients of block 1 (its attention gets gradient on query 0 only), so the scale of each
-    tensor's gate is the larger of their two errors.  Train mode uses the same counter-hash dropout masks in all
-    (element-exact mask parity)."""
+
+    Tolerance scale: the spread of VALID bf16 evaluations, each rounding to bf16 at this path's storage points —
+    the oracle with fp32 arithmetic between them, the same with fp64, and the same with the MFMA flash-attention
+    kernels' internal roundings (oracle `flash=True`: P and dS in bf16).  Gates:
+      * logits within 1e-2 (norm-wise) of the bf16 oracle;
+      * every gradient except the attention query / key projections: error vs the fp32 oracle <= max(3e-2, 2 x the
+        largest error of a valid evaluation);
+      * query / key projection gradients, per block with all heads concatenated: the same gate.  Per head they are
+        chaotic under the saturating x sqrt(hd) softmax — block 1's attention gets gradient on query 0 only (the
+        classifier reads token 0), and two valid evaluations differ by 10-200% on single heads (measured);
+      * the whole gradient vector: <= max(1e-2, 2 x the largest valid error).
+    Train mode uses the same counter-hash dropout masks in all evaluations (element-exact mask parity)."""
     ocfg = O.make_config("base", img=224, batch=2, blocks=2, num_classes=1000)
     st = O.init_state(ocfg, seed=21)
     m = _model(ocfg, st, torch.bfloat16).train(train)
@@ -71,26 +76,36 @@ def test_base_width_bf16_engine_vs_oracle(train):
     logits = m(x.to(DEV))
     loss = cross_entropy(logits, y.to(DEV))
     loss.backward()
+    ours = {k: p.grad.cpu().double() for k, p in m.named_parameters()}
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    lg_bf, _, g_bf = O.loss_and_grads(st, x, y, ocfg, bf16=True, train=train, seed=base_seed)
-    _, _, g_b64 = O.loss_and_grads(st, x, y, ocfg, bf16=True, dtype=torch.float64, train=train, seed=base_seed)
-    lg_32, _, g_32 = O.loss_and_grads(st, x, y, ocfg, train=train, seed=base_seed)
+    kw = dict(train=train, seed=base_seed)
+    lg_bf, _, g_bf = O.loss_and_grads(st, x, y, ocfg, bf16=True, **kw)
+    _, _, g_32 = O.loss_and_grads(st, x, y, ocfg, **kw)
+    valid = [g_bf, O.loss_and_grads(st, x, y, ocfg, bf16=True, dtype=torch.float64, **kw)[2],
+             O.loss_and_grads(st, x, y, ocfg, bf16=True, flash=True, **kw)[2]]
     assert _rel(logits.detach().cpu(), lg_bf) < 1e-2
+
+    def err(g, keys):
+        a = torch.cat([g[k].reshape(-1).double() for k in keys])
+        r = torch.cat([g_32[k].reshape(-1).double() for k in keys])
+        return float((a - r).norm() / r.norm())
+
+    groups = {}
+    for k in g_32:
+        if ".query." in k or ".key." in k:
+            groups.setdefault(k.split(".multi_head")[0] + " q/k (all heads)", []).append(k)
+        else:
+            groups[k] = [k]
+    groups["ALL"] = list(g_32)
     bad, worst = [], []
-    for k, p in m.named_parameters():
-        ours = _rel(p.grad.cpu(), g_32[k])
-        ora = max(_rel(g_bf[k], g_32[k]), _rel(g_b64[k].float(), g_32[k]))
-        worst.append((ours / max(ora, 1e-9), k, ours, ora))
-        if ours > max(3e-2, 2 * ora):
-            bad.append((k, ours, ora))
-    print("worst grad error ratios:", sorted(worst)[-3:])
+    for name, keys in groups.items():
+        e_ours = err(ours, keys)
+        e_ora = max(err(v, keys) for v in valid)
+        worst.append((e_ours / max(e_ora, 1e-9), name, e_ours, e_ora))
+        if e_ours > max(1e-2 if name == "ALL" else 3e-2, 2 * e_ora):
+            bad.append((name, e_ours, e_ora))
+    print("worst error ratios:", sorted(worst)[-4:])
     assert not bad, bad
-    cat = lambda gs: torch.cat([gs[k].reshape(-1).double() for k in g_32])
-    ours_all = torch.cat([p.grad.cpu().reshape(-1).double() for _, p in m.named_parameters()])
-    e_ours = float((ours_all - cat(g_32)).norm() / cat(g_32).norm())
-    e_ora = max(float((cat(g_bf) - cat(g_32)).norm() / cat(g_32).norm()),
-                float((cat(g_b64) - cat(g_32)).norm() / cat(g_32).norm()))
-    assert e_ours <= max(1e-2, 2 * e_ora), (e_ours, e_ora)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

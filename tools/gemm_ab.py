@@ -1,0 +1,121 @@
+"""Interleaved A/B of libvit_hip.so builds on the ViT GEMM shapes (one process, rounds alternate between builds:
+cdna_hip_programming.md §5.4 rule 24).  Each build is loaded RTLD_LOCAL, so several coexist.
+
+    python tools/gemm_ab.py LIB1.so LIB2.so@VIT_GEMM_GROUP=4 ... [--reps 10] [--shapes fwd_qkv,...]
+
+A build spec may carry `@NAME=VALUE[,NAME=VALUE]`: environment set around that build's calls (runtime switches such as
+VIT_GEMM_GROUP).  Prints the median time per (shape, build) and TF/s; checks outputs bitwise against the first.""" 
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vision-transformer_amd"))
+import torch  # noqa: E402
+from VisionTransformer import _lib  # noqa: E402  (GemmDesc layout)
+
+M, D = 256 * 197, 768
+SHAPES = {  # name: m, n, k, a_kcontig, b_kcontig, epilogue
+    "fwd_qkv": (M, 3 * D, D, True, True, None), "fwd_proj": (M, D, D, True, True, "bdr"),
+    "fwd_fc1": (M, 4 * D, D, True, True, "bias_relu"), "fwd_fc2": (M, D, 4 * D, True, True, "bdr"),
+    "dgrad_fc2": (M, 4 * D, D, True, False, "aux"), "dgrad_fc1": (M, D, 4 * D, True, False, None),
+    "dgrad_qkv": (M, D, 3 * D, True, False, None), "dgrad_proj": (M, D, D, True, False, None),
+    "wgrad_fc1": (4 * D, D, M, False, False, "wgrad"), "wgrad_fc2": (D, 4 * D, M, False, False, "wgrad"),
+    "wgrad_qkv": (3 * D, D, M, False, False, "wgrad"), "wgrad_proj": (D, D, M, False, False, "wgrad"),
+    "sq8192": (8192, 8192, 8192, True, True, None),
+}
+
+
+def load(path):
+    lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL)
+    lib.vit_gemm.argtypes = [ctypes.POINTER(_lib.GemmDesc), ctypes.c_void_p]
+    lib.vit_gemm_workspace_bytes.argtypes = [ctypes.POINTER(_lib.GemmDesc)]
+    lib.vit_gemm_workspace_bytes.restype = ctypes.c_int64
+    lib.vit_gemm_split_k_hint.argtypes = [ctypes.c_int64] * 3 + [ctypes.c_int]
+    lib.vit_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res):
+    d = _lib.GemmDesc()
+    d.a, d.b, d.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
+    d.lda, d.ldb, d.ldc = a.stride(0), b.stride(0), n
+    d.m, d.n, d.k = m, n, k
+    d.a_kcontig, d.b_kcontig = int(akc), int(bkc)
+    d.in_dtype = _lib.BF16
+    d.out_dtype = _lib.F32 if epi == "wgrad" else _lib.BF16
+    d.alpha, d.beta = 1.0, 0.0
+    if epi in ("bias_relu", "bdr"):
+        d.bias = bias.data_ptr()
+    if epi == "bias_relu":
+        d.act = _lib.ACT_RELU
+    if epi == "aux":
+        d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), n, _lib.BF16
+    if epi == "bdr":
+        d.res, d.ldres, d.res_dtype = res.data_ptr(), n, _lib.BF16
+        d.dropout_p, d.dropout_seed = 0.2, 7
+    d.split_k = split
+    d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    args = ap.parse_args()
+    specs = [(s.split("@")[0], dict(kv.split("=") for kv in s.split("@")[1].split(",")) if "@" in s else {})
+             for s in args.libs]
+    cache = {}
+    libs = [cache.setdefault(p, load(p)) for p, _ in specs]
+    envs = [e for _, e in specs]
+    names = [os.path.basename(p).replace("libvit_hip_", "").replace(".so", "") +
+             ("@" + ",".join(f"{k}={v}" for k, v in e.items()) if e else "") for p, e in specs]
+    ws = torch.empty(96 << 20, dtype=torch.float32, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for sname in args.shapes.split(","):
+        m, n, k, akc, bkc, epi = SHAPES[sname]
+        a = (torch.rand((m, k) if akc else (k, m), device="cuda", generator=g) * 2 - 1).bfloat16()
+        b = (torch.rand((n, k) if bkc else (k, n), device="cuda", generator=g) * 2 - 1).bfloat16()
+        aux = (torch.rand(m, n, device="cuda", generator=g) - 0.3).bfloat16()
+        res = torch.randn(m, n, device="cuda", generator=g).bfloat16()
+        bias = torch.randn(n, device="cuda", generator=g)
+        c = torch.empty(m, n, dtype=torch.float32 if epi == "wgrad" else torch.bfloat16, device="cuda")
+        split = libs[0].vit_gemm_split_k_hint(m, n, k, _lib.BF16) if epi == "wgrad" else 1
+        times = {nm: [] for nm in names}
+        outs = {}
+        for rep in range(args.reps + 2):
+            for nm, lib, env in zip(names, libs, envs):
+                saved = {kk: os.environ.get(kk) for kk in env}
+                os.environ.update(env)
+                d = desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc = lib.vit_gemm(ctypes.byref(d), stream)
+                e1.record()
+                torch.cuda.synchronize()
+                for kk, vv in saved.items():
+                    if vv is None:
+                        os.environ.pop(kk, None)
+                    else:
+                        os.environ[kk] = vv
+                if rc != 0:
+                    sys.exit(f"{nm}: vit_gemm failed: {lib.vit_last_error().decode()}")
+                if rep >= 2:
+                    times[nm].append(e0.elapsed_time(e1) / 1e3)
+                if rep == 2:
+                    outs[nm] = c.clone()
+        flop = 2.0 * m * n * k
+        line = f"{sname:10s} split={split:2d}"
+        for nm in names:
+            t = sorted(times[nm])[len(times[nm]) // 2]
+            same = "=" if torch.equal(outs[nm], outs[names[0]]) else "!"
+            line += f" | {nm}: {t * 1e6:7.1f}us {flop / t / 1e12:7.1f}TF {same}"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()

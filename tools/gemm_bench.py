@@ -22,7 +22,7 @@ SHAPES = [  # name, m, n, k, a_kcontig, b_kcontig  (C = A(i,r) B(j,r))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--impls", default="2,3")
+    ap.add_argument("--impls", default="4")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--no-ref", action="store_true", help="skip the hipBLASLt row")

@@ -295,9 +295,9 @@ class Engine:
         if h is not None:
             h(fam, phase, flop, nbytes)
 
-    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta, side=None, fam=None):
-        """out[m][n] (+)= sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K.  With `side` it
-        runs on that stream after everything already enqueued on the current one."""
+    def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta, side=None, fam=None, alpha=1.0):
+        """out[m][n] (+)= alpha sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K.  With `side`
+        it runs on that stream after everything already enqueued on the current one."""
         split = split_k_for(m, n, k, dy.dtype)
         need = split * m * n * 4 if split > 1 else 0
         if side is None:
@@ -305,7 +305,7 @@ class Engine:
             if fam:
                 self._mark(fam, 0, 2.0 * m * n * k, (m + n) * k * dy.element_size() + m * n * 4 * (1 + (beta != 0)))
             _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
-                      split_k=split, workspace=ws)
+                      alpha=alpha, split_k=split, workspace=ws)
             if fam:
                 self._mark(fam, 1)
             return
@@ -316,7 +316,7 @@ class Engine:
                 self._wws = torch.empty(max(need // 4 + 1, 1 << 20), dtype=torch.float32, device=self.device)
             ws = self._wws
         _ops.gemm(dy, x, out, m, n, k, ld_dy, ld_x, out.stride(0), a_kcontig=False, b_kcontig=False, beta=beta,
-                  split_k=split, workspace=ws, stream=side)
+                  alpha=alpha, split_k=split, workspace=ws, stream=side)
         for t in (dy, x) if ws is None else (dy, x, ws):
             t.record_stream(side)          # the caching allocator must not hand these out before `side` is done
 
@@ -332,8 +332,8 @@ class Engine:
         self._head_gemm(x, w, y, m, n, k, x.stride(0), w.stride(0), n, bias=bias)
         return y
 
-    def _colsum(self, x, rows, cols, ld, out, beta):
-        _ops.colsum(x, rows, cols, ld, out, beta=beta)
+    def _colsum(self, x, rows, cols, ld, out, beta, alpha=1.0):
+        _ops.colsum(x, rows, cols, ld, out, beta=beta, alpha=alpha)
 
     def _attach_grads(self):
         """Expose the flat gradient buffer as param.grad of every parameter that requires grad (frozen ones keep
@@ -524,9 +524,12 @@ class Engine:
         # ---- d(encoder output): only token-0 rows are nonzero
         dx = torch.zeros(M, D, dtype=dt, device=dev)
         _ops.copy2d(dz, D, dx, T * D, B, D)
+        # Dropout backward as a bare mask (exact in bf16); its 1/(1-p) goes into every consumer of the masked gradient
+        # (GEMM alpha, column-sum alpha, the LN kernels' bias-gradient sums) instead of a rounding of its own.
+        gs = 1.0 / (1.0 - DROPOUT_P) if tape.training else 1.0
         g1 = torch.empty_like(dx)
         if tape.training:
-            _ops.dropout_bwd(dx, g1, DROPOUT_P, site_seed(tape.seed, L - 1, 1))
+            _ops.dropout_bwd(dx, g1, DROPOUT_P, site_seed(tape.seed, L - 1, 1), scale=1.0)
         else:
             g1 = dx
         side = self._side_stream()
@@ -537,15 +540,15 @@ class Engine:
             x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h = tape.blocks[l]
             # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
             if req[f"{l}.fc2_w"]:
-                self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side, "gemm_wgrad")
+                self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side, "gemm_wgrad", alpha=gs)
             if not g1_summed:
-                self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta)
+                self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta, alpha=gs)
             dh = torch.empty(M, 4 * D, dtype=dt, device=dev)
             dh_part = torch.empty(_ops.colsum_part_rows(M), 4 * D, dtype=torch.float32, device=dev)
             # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
             mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 8 * M * D) * es)
             _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=h,
-                      ldaux=4 * D, colsum_part=dh_part)
+                      ldaux=4 * D, colsum_part=dh_part, alpha=gs)
             mk("gemm_dgrad", 1)
             _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
             if req[f"{l}.fc1_w"]:
@@ -567,10 +570,10 @@ class Engine:
                 g0 = dx_mid
             # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
             if req[f"{l}.proj_w"]:
-                self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta, side, "gemm_wgrad")
+                self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta, side, "gemm_wgrad", alpha=gs)
             do = torch.empty(M, D, dtype=dt, device=dev)
             mk("gemm_dgrad", 0, 2.0 * M * D * D, (2 * M * D + D * D) * es)
-            _ops.gemm(g0, self.ww[f"{l}.proj_w"], do, M, D, D, D, D, D, b_kcontig=False)
+            _ops.gemm(g0, self.ww[f"{l}.proj_w"], do, M, D, D, D, D, D, b_kcontig=False, alpha=gs)
             mk("gemm_dgrad", 1)
             mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 8 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                           else 0))

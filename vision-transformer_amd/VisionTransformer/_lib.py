@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
@@ -62,10 +62,10 @@ _SIGS = {
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
     "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _P]),
     "vit_colsum_workspace_bytes": (_I64, [_I64, _I64]),
-    "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _P, _P]),
+    "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _F, _P, _P]),
     "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),
     "vit_copy2d": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _I32, _I64, _I64, _I64, _I64, _F, _P]),
-    "vit_dropout_bwd": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _U32, _P]),
+    "vit_dropout_bwd": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _U32, _F, _P]),
     "vit_relu_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _P]),
     "vit_gelu_fwd": (ctypes.c_int, [_P, _P, _I64, _P]),
     "vit_gelu_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),

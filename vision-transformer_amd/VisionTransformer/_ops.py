@@ -126,9 +126,10 @@ def layernorm_bwd_parts(rows, cols):
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, drop_p=0.0, drop_seed=0,
                   partial=None, osum=False, stream=None):
-    """dx_out = LN_bwd(dy) (+ dres); drop_out = dropout_bwd(dx_out); returns partial [2, parts, cols] f32
-    (dgamma / dbeta per workgroup) — [3, parts, cols] with `osum`: + the column sums of the stored gradient output
-    (drop_out when given, else dx_out), i.e. the bias gradient of the Linear it feeds.  Reduce with colsum_finish."""
+    """dx_out = LN_bwd(dy) (+ dres); drop_out = dx_out * keep (UNSCALED: consumers multiply by 1/(1-p)); returns
+    partial [2, parts, cols] f32 (dgamma / dbeta per workgroup) — [3, parts, cols] with `osum`: + the column sums of
+    the gradient the next Linear sees (drop_out / (1-p) when given, else dx_out), i.e. its bias gradient.  Reduce
+    with colsum_finish."""
     rows, cols = x.shape
     parts = layernorm_bwd_parts(rows, cols)
     if partial is None:
@@ -164,11 +165,11 @@ def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, o3
     return dqkv
 
 
-def colsum(x, rows, cols, ldx, out, beta=0.0, workspace=None, stream=None):
+def colsum(x, rows, cols, ldx, out, beta=0.0, workspace=None, alpha=1.0, stream=None):
     need = _lib.load().vit_colsum_workspace_bytes(rows, cols)
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty(max(need // 4, 1), dtype=torch.float32, device=x.device)
-    _lib.call("vit_colsum", _ptr(x), ldx, dtype_code(x), rows, cols, _ptr(out), beta, _ptr(workspace),
+    _lib.call("vit_colsum", _ptr(x), ldx, dtype_code(x), rows, cols, _ptr(out), alpha, beta, _ptr(workspace),
               _stream(stream))
     return out
 
@@ -194,8 +195,11 @@ def copy2d(src, lds, dst, ldd, rows, cols, group=(0, 0), beta=0.0, stream=None):
     return dst
 
 
-def dropout_bwd(x, y, p, seed, stream=None):
-    _lib.call("vit_dropout_bwd", _ptr(x), _ptr(y), dtype_code(x), x.numel(), p, seed & 0xFFFFFFFF, _stream(stream))
+def dropout_bwd(x, y, p, seed, scale=None, stream=None):
+    """y = x * keep * scale (scale defaults to 1/(1-p))."""
+    scale = 1.0 / (1.0 - p) if scale is None else scale
+    _lib.call("vit_dropout_bwd", _ptr(x), _ptr(y), dtype_code(x), x.numel(), p, seed & 0xFFFFFFFF, scale,
+              _stream(stream))
     return y
 
 

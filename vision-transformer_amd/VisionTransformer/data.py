@@ -222,6 +222,20 @@ class DeviceBatches:
             yield x, y
 
 
+class Transformed(torch.utils.data.Dataset):
+    """(item, label) dataset with a per-item transform (the host path's Compose)."""
+
+    def __init__(self, ds, tf):
+        self.ds, self.tf = ds, tf
+
+    def __len__(self):
+        return len(self.ds)
+
+    def __getitem__(self, i):
+        x, y = self.ds[i]
+        return self.tf(x), y
+
+
 def host_transform(size):
     """The reference transform on the host (Pillow): convert('RGB') -> resize((S, S), BILINEAR) -> /255 CHW."""
     sh, sw = (size, size) if isinstance(size, int) else size

@@ -524,7 +524,7 @@ VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_
     return;
   }
   if (KIND == EPI_SLAB) {
-    slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
+    slab_store4(g.ws, g.M, g.N, i, j, v);          // g.ws: this workgroup's K-slice slab (set by the kernel)
     return;
   }
   if (i >= e.m || j >= e.n) return;                 // fast kinds: n % 4 == 0 and 16-B aligned rows (e.vec)
@@ -687,9 +687,17 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
+  // One-dimensional grid of tiles x K-slices.  Workgroups are dealt round-robin over the 8 XCDs (linear id % 8); the
+  // bijective remap gives each XCD a contiguous range of `bid`, and bid is split-major (all tiles of K-slice 0, then
+  // slice 1, ...), so the ~32 workgroups an XCD runs at once are tiles of ONE K-slice that share A row panels and B
+  // column panels, walking k in step: the XCD's L2 serves the re-reads.  (With the slices on gridDim.y the hardware's
+  // linear order x + y * gridDim.x scattered a panel's tiles over XCDs: the weight-gradient GEMMs fetched ~3.5x their
+  // operand bytes from beyond L2.)
   const int64_t nwg = gridDim.x, orig = blockIdx.x;
   const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t bid_all = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int64_t ntile = g.tiles_m * g.tiles_n;
+  const int64_t sidx = bid_all / ntile, bid = bid_all % ntile;
   int64_t tm, tn;
   if (g.group_m > 1) {
     // L2 locality: the ~32 tiles an XCD runs at once span group_m A panels x 32/group_m B panels
@@ -701,9 +709,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     tm = bid / g.tiles_n;
     tn = bid % g.tiles_n;
   }
+  if (g.ws) g.ws += sidx * g.M * g.N;                  // this K-slice's fp32 slab (EPI_SLAB)
   const int64_t i0 = tm * 256, j0 = tn * 256;
   const int64_t nkt = g.K / BK;
-  const int64_t kt0 = (int64_t)blockIdx.y * g.kt_per_split;
+  const int64_t kt0 = sidx * g.kt_per_split;
   const int nk = (int)max((int64_t)0, min(nkt, kt0 + g.kt_per_split) - kt0);
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
@@ -758,40 +767,75 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   if (wr == 1) __builtin_amdgcn_s_barrier();              // group 1 runs one barrier behind group 0
 
   bf16x8_t af[4][2], b0f[2][2], b1f[2][2];
-  for (int t = 0; t < nk; ++t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 4 * t + r;
-      if (r == 0) {
-        read_a4<AKC, BKC>(V4_SLOT(4 * t), wr, lane, af);
-        read_b4<BKC>(V4_SLOT(4 * t + 1), wc, lane, b0f);
-      } else if (r == 1) {
-        read_b4<BKC>(V4_SLOT(4 * t + 2), wc, lane, b1f);
-      } else if (r == 2) {
-        read_a4<AKC, BKC>(V4_SLOT(4 * t + 3), wr, lane, af);
-      }
+  // One phase f = 4t + r.  STEADY: the k-tiles before the last two, where every phase issues its DMA stage and the
+  // retiring wait is the constant vmcnt(2 * (LEAD - 2)) — no per-phase branches (the tail's counts are computed).
 #ifndef VIT_V4_NODMA
-      if (f + V4_LEAD < nstage) V4_STAGE(f + V4_LEAD);
-      wait_stage_retired(min(V4_LEAD - 2, nstage - 1 - (f + 2)));
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-#ifdef VIT_V4_NOMFMA
-      if (r == 0) { asm volatile("" ::"v"(af[0][0]), "v"(af[3][1]), "v"(b0f[0][0]), "v"(b0f[1][1])); }
-      else if (r == 1) { asm volatile("" ::"v"(b1f[0][0]), "v"(b1f[1][1])); }
-      else if (r == 2) { asm volatile("" ::"v"(af[0][0]), "v"(af[3][1])); }
+#define V4_PHASE_DMA(F, STEADY)                                                                  \
+  do {                                                                                           \
+    if (STEADY) {                                                                                \
+      V4_STAGE((F) + V4_LEAD);                                                                   \
+      wait_stage_retired(V4_LEAD - 2);                                                           \
+    } else {                                                                                     \
+      if ((F) + V4_LEAD < nstage) V4_STAGE((F) + V4_LEAD);                                       \
+      wait_stage_retired(min(V4_LEAD - 2, nstage - 1 - ((F) + 2)));                              \
+    }                                                                                            \
+  } while (0)
 #else
-      if (r == 0) mfma_quadrant(acc[0][0], af, b0f);
-      else if (r == 1) mfma_quadrant(acc[0][1], af, b1f);
-      else if (r == 2) mfma_quadrant(acc[1][1], af, b1f);
-      else mfma_quadrant(acc[1][0], af, b0f);
+#define V4_PHASE_DMA(F, STEADY) do {} while (0)
 #endif
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
+#ifdef VIT_V4_NOMFMA
+#define V4_PHASE_MFMA(R)                                                                         \
+  do {                                                                                           \
+    if ((R) == 0) { asm volatile("" ::"v"(af[0][0]), "v"(af[3][1]), "v"(b0f[0][0]), "v"(b0f[1][1])); } \
+    else if ((R) == 1) { asm volatile("" ::"v"(b1f[0][0]), "v"(b1f[1][1])); }                    \
+    else if ((R) == 2) { asm volatile("" ::"v"(af[0][0]), "v"(af[3][1])); }                       \
+  } while (0)
+#else
+#define V4_PHASE_MFMA(R)                                                                         \
+  do {                                                                                           \
+    if ((R) == 0) mfma_quadrant(acc[0][0], af, b0f);                                             \
+    else if ((R) == 1) mfma_quadrant(acc[0][1], af, b1f);                                        \
+    else if ((R) == 2) mfma_quadrant(acc[1][1], af, b1f);                                        \
+    else mfma_quadrant(acc[1][0], af, b0f);                                                      \
+  } while (0)
+#endif
+#define V4_PHASE(T, R, STEADY)                                                                   \
+  do {                                                                                           \
+    const int f_ = 4 * (T) + (R);                                                                \
+    if ((R) == 0) {                                                                              \
+      read_a4<AKC, BKC>(V4_SLOT(4 * (T)), wr, lane, af);                                         \
+      read_b4<BKC>(V4_SLOT(4 * (T) + 1), wc, lane, b0f);                                         \
+    } else if ((R) == 1) {                                                                       \
+      read_b4<BKC>(V4_SLOT(4 * (T) + 2), wc, lane, b1f);                                         \
+    } else if ((R) == 2) {                                                                       \
+      read_a4<AKC, BKC>(V4_SLOT(4 * (T) + 3), wr, lane, af);                                     \
+    }                                                                                            \
+    V4_PHASE_DMA(f_, STEADY);                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    __builtin_amdgcn_s_barrier();                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    V4_PHASE_MFMA(R);                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    __builtin_amdgcn_s_barrier();                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+  } while (0)
+  const int nsteady = nk > 2 ? nk - 2 : 0;            // LEAD in [4, 8]: phases of k-tiles < nk - 2 are steady
+  int t = 0;
+  for (; t < nsteady; ++t) {
+    V4_PHASE(t, 0, true);
+    V4_PHASE(t, 1, true);
+    V4_PHASE(t, 2, true);
+    V4_PHASE(t, 3, true);
   }
+  for (; t < nk; ++t) {
+    V4_PHASE(t, 0, false);
+    V4_PHASE(t, 1, false);
+    V4_PHASE(t, 2, false);
+    V4_PHASE(t, 3, false);
+  }
+#undef V4_PHASE
+#undef V4_PHASE_MFMA
+#undef V4_PHASE_DMA
 #undef V4_STAGE
 #undef V4_SLOT
 #undef V4_DMA
@@ -1104,12 +1148,15 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     g4.tiles_n = (d->n + 255) / 256;
     g4.tiles_m = (d->m + 255) / 256;
     {
+      // Tile order inside an XCD's contiguous range: with many tile columns, row-major order puts ONE A panel and ~32
+      // B panels on an XCD at once (little L2 reuse); groups of 8 tile rows, column-major inside a group, give ~8 x 4.
+      // Measured (tools/gemm_ab.py): 8192^3 1146 -> 1566 TF/s; neutral on the ViT shapes (<= 12 tile columns).
       const char* gv = getenv("VIT_GEMM_GROUP");
-      g4.group_m = gv ? atoi(gv) : 1;
+      g4.group_m = gv ? atoi(gv) : (g4.tiles_n >= 16 ? 8 : 1);
       if (g4.group_m < 1) g4.group_m = 1;
     }
     g4.kt_per_split = (nkt + split - 1) / split;
-    dim3 grid4((unsigned)(((d->m + 255) / 256) * g4.tiles_n), (unsigned)split);
+    dim3 grid4((unsigned)(((d->m + 255) / 256) * g4.tiles_n * split), 1u);   // tiles x K-slices, split-major
     // v4 epilogue kind
     const bool fast = e.vec && e.grp == 0 && e.res_rowmod == 0 && e.beta == 0.f;
     int kind = EPI_GENERAL;

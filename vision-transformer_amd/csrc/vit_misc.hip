@@ -86,7 +86,7 @@ constexpr int CS_CHUNKS_MAX = 256;
 template <class T>
 __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ x, int64_t ldx, int64_t rows,
                                                      int64_t cols, int64_t rows_per_chunk, float* __restrict__ part,
-                                                     int vec) {
+                                                     int vec, float alpha = 1.f) {
   __shared__ float red[4][256];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * 256 + tx * 4;
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(256) void colsum_stage1(const T* __restrict__ x, in
     for (int k = 0; k < 4; ++k) {
       const int cc = tx * 4 + k;
       const float s = red[0][cc] + red[1][cc] + red[2][cc] + red[3][cc];
-      if (c0 + k < cols) part[chunk * cols + c0 + k] = s;
+      if (c0 + k < cols) part[chunk * cols + c0 + k] = s * alpha;
     }
   }
 }
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void copy2d_kernel(const TS* __restrict__ src,
 
 template <class T>
 __global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
-                                                          uint32_t thr, float scale, uint32_t seed) {
+                                                          uint32_t thr, float scale, uint32_t seed) {  // y = keep*x*scale
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
     const float v = ld1<T>(x + t);
     st1<T>(y + t, vit_hash_u32(seed, (uint32_t)t) >= thr ? v * scale : 0.f);
@@ -357,7 +357,7 @@ extern "C" int64_t vit_colsum_workspace_bytes(int64_t rows, int64_t cols) {
 }
 
 extern "C" int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t cols, float* out,
-                          float beta, void* workspace, void* stream) {
+                          float alpha, float beta, void* workspace, void* stream) {
   VIT_REQUIRE(x && out && workspace && rows > 0 && cols > 0, "vit_colsum: bad arguments");
   const int64_t ch = colsum_chunks(rows, cols);
   const int64_t rpc = (rows + ch - 1) / ch;
@@ -365,9 +365,9 @@ extern "C" int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t row
   dim3 g1((unsigned)((cols + 255) / 256), (unsigned)ch);
   hipStream_t s = VIT_STREAM(stream);
   if (dtype == VIT_BF16)
-    colsum_stage1<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
+    colsum_stage1<bf16_t><<<g1, 256, 0, s>>>((const bf16_t*)x, ldx, rows, cols, rpc, (float*)workspace, vec, alpha);
   else
-    colsum_stage1<float><<<g1, 256, 0, s>>>((const float*)x, ldx, rows, cols, rpc, (float*)workspace, vec);
+    colsum_stage1<float><<<g1, 256, 0, s>>>((const float*)x, ldx, rows, cols, rpc, (float*)workspace, vec, alpha);
   OutSet outs{{out, nullptr, nullptr}};
   colsum_stage2<<<(unsigned)((cols + 63) / 64), 64 * CS2_WAVES, 0, s>>>((const float*)workspace, ch, cols, outs, beta);
   return vit::check_launch("vit_colsum");
@@ -400,12 +400,11 @@ extern "C" int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void*
   return vit::check_launch("vit_copy2d");
 }
 
-extern "C" int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed,
+extern "C" int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, uint32_t seed, float scale,
                                void* stream) {
   VIT_REQUIRE(x && y && n > 0 && p >= 0.f && p < 1.f, "vit_dropout_bwd: bad arguments");
   double t = (double)p * 4294967296.0;
   const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
-  const float scale = 1.0f / (1.0f - p);
   const unsigned grid = grid_for(n, 256, 16384);
   hipStream_t s = VIT_STREAM(stream);
   if (dtype == VIT_BF16) dropout_bwd_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, thr, scale, seed);

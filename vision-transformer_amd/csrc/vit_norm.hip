@@ -129,16 +129,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
         for (int r = 0; r < 4; ++r) o[r] = rs * (dv[k][r] - a - xv[k][r] * b) + rv[k][r];
         st4<T>(dx_out + row * cols + c, o);
         if (drop_out) {
-          // drop the value as stored (rounded), matching a separate dropout-backward pass over dx_out
+          // the dropout mask on the value as stored, WITHOUT the 1/(1-p) scale: exact in any dtype (the scale is
+          // applied by the consumers — GEMM alpha, and the column sums below), so the masked gradient adds no
+          // rounding of its own
           const uint32_t base = (uint32_t)(row * cols + c);
           float dd[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? as_stored<T>(o[r]) * drop_scale : 0.f;
+          for (int r = 0; r < 4; ++r) dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? as_stored<T>(o[r]) : 0.f;
           st4<T>(drop_out + row * cols + c, dd);
           if (osum) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) os[k][r] += as_stored<T>(dd[r]);
+            for (int r = 0; r < 4; ++r) os[k][r] += dd[r];
           }
         } else if (osum) {
 #pragma unroll
@@ -170,8 +171,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
     __syncthreads();
   }
   const int nset = osum ? 3 : 2;
+  const float oscale = drop_out ? drop_scale : 1.f;   // set 2 = column sums of drop_out * 1/(1-p)
   for (int64_t c = threadIdx.x; c < cols; c += 256)
-    for (int s = 0; s < nset; ++s) partial[(s * parts + blockIdx.x) * cols + c] = red[s][c];
+    for (int s = 0; s < nset; ++s) partial[(s * parts + blockIdx.x) * cols + c] = s == 2 ? red[s][c] * oscale : red[s][c];
 }
 
 template <int NV, class T>

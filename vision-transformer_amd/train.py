@@ -13,8 +13,11 @@ torch ops on all host cores, torch.optim.AdamW) — the reference's own behaviou
 
 Differences (documented in DESIGN.md): hyper-parameters come from flags instead of hard-coded constants (the
 reference's TODO at :124-125); data defaults to a synthetic CIFAR-shaped stream because the container has no network
-(CIFAR10(download=True) at :157-159 cannot run) — `--cifar-root` uses torchvision's CIFAR10 when it is installed and
-the files are present; tensorboard is used when importable, else scalars go to a JSONL file.
+(CIFAR10(download=True) at :157-159 cannot run).  `--data cifar10-bin --data-root R` reads CIFAR-10's binary batches,
+`--data folder --data-root R` a folder-per-class image tree (BrainTumorDataset.py), `--data synthetic-u8` random uint8
+images; on the GPU those run the reference transform (convert RGB -> Resize((S, S)) -> ToTensor, train.py:151-155)
+as one kernel per batch (VisionTransformer/data.py, bit-exact with Pillow), on the host with Pillow per image.
+tensorboard is used when importable, else scalars go to a JSONL file.
 """
 import argparse
 import glob
@@ -208,7 +211,10 @@ def main():
     ap.add_argument("--test-size", type=int, default=64)
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--eval-iter", type=int, default=1)
-    ap.add_argument("--cifar-root", default=None)
+    ap.add_argument("--data", default="synthetic", choices=["synthetic", "synthetic-u8", "cifar10-bin", "folder"],
+                    help="synthetic: N(0,1) float images at --img; the others decode uint8 images and apply the "
+                         "reference transform (GPU kernel on cuda, Pillow on cpu)")
+    ap.add_argument("--data-root", default=None)
     ap.add_argument("--checkpoint-dir", default="../checkpoints")
     ap.add_argument("--log-dir", default="../logs")
     ap.add_argument("--workers", type=int, default=2)
@@ -247,22 +253,37 @@ def main():
                           "steps": steps, "ms_per_step": round(sec * 1e3, 3),
                           "images_per_s": round(args.batch / sec, 3), "final_loss": round(last, 5)}), flush=True)
         return
-    if args.cifar_root:
-        import torchvision.transforms as transforms
-        from torchvision.datasets import CIFAR10
-        tf = transforms.Compose([transforms.Resize((args.img, args.img)), transforms.ToTensor()])
-        train_set = CIFAR10(root=args.cifar_root, download=False, transform=tf)
-        test_set = CIFAR10(root=args.cifar_root, download=False, train=False, transform=tf)
-    else:
+    pin = device == "cuda"
+    if args.data == "synthetic":
         train_set = SyntheticImages(args.train_size, 3, args.img, args.classes, seed=1 + rank)
         test_set = SyntheticImages(args.test_size, 3, args.img, args.classes, seed=10_000)
+    else:
+        from VisionTransformer import data as D
+        if args.data == "cifar10-bin":
+            train_set, test_set = D.CIFAR10Bin(args.data_root, True), D.CIFAR10Bin(args.data_root, False)
+        elif args.data == "folder":
+            train_set = D.BrainTumorDataset(args.data_root, train=True, transform=D.decode)
+            test_set = D.BrainTumorDataset(args.data_root, train=False, transform=D.decode)
+        else:
+            train_set = D.SyntheticRawImages(args.train_size, (32, 32, 3), args.classes, seed=1 + rank)
+            test_set = D.SyntheticRawImages(args.test_size, (32, 32, 3), args.classes, seed=10_000)
     sampler = torch.utils.data.DistributedSampler(train_set) if world > 1 else None
-    pin = device == "cuda"
-    train_loader = torch.utils.data.DataLoader(train_set, batch_size=args.batch, shuffle=sampler is None,
-                                               sampler=sampler, num_workers=args.workers, drop_last=True,
-                                               pin_memory=pin)
-    test_loader = torch.utils.data.DataLoader(test_set, batch_size=args.batch, num_workers=args.workers,
-                                              drop_last=True, pin_memory=pin)
+    if args.data != "synthetic" and device == "cuda":
+        from VisionTransformer import data as D
+        tf = D.GpuImageTransform(args.img)
+        train_loader = D.DeviceBatches(D.raw_loader(train_set, args.batch, shuffle=True, num_workers=args.workers,
+                                                    sampler=sampler), tf, device)
+        test_loader = D.DeviceBatches(D.raw_loader(test_set, args.batch, shuffle=False, num_workers=args.workers),
+                                      tf, device)
+    else:
+        if args.data != "synthetic":
+            from VisionTransformer import data as D
+            train_set, test_set = (D.Transformed(s, D.host_transform(args.img)) for s in (train_set, test_set))
+        train_loader = torch.utils.data.DataLoader(train_set, batch_size=args.batch, shuffle=sampler is None,
+                                                   sampler=sampler, num_workers=args.workers, drop_last=True,
+                                                   pin_memory=pin)
+        test_loader = torch.utils.data.DataLoader(test_set, batch_size=args.batch, num_workers=args.workers,
+                                                  drop_last=True, pin_memory=pin)
     train(cfg, train_loader, test_loader, args.epochs, args.eval_iter, args.log_dir, args.checkpoint_dir,
           lr=args.lr, max_steps=args.steps)
     if world > 1:
