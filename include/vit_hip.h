@@ -22,10 +22,14 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 5
+#define VIT_ABI_VERSION 6
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
-typedef enum { VIT_F32 = 0, VIT_BF16 = 1 } vit_dtype;
+typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
+
+/* VIT_MASK4: a bit mask of an [m][n] tensor (ReLU / dropout masks saved by the forward for the backward): byte
+ * ((i/4)*ceil(n/4) + j/4)*4 + i%4, bit j%4; 4*ceil(m/4)*ceil(n/4) bytes.  One byte = 4 columns of a row; one dword =
+ * a 4 x 4 block (byte = row).  8x smaller than the bf16 tensor it replaces as a mask source. */
 typedef enum { VIT_ACT_NONE = 0, VIT_ACT_RELU = 1, VIT_ACT_GELU = 2 } vit_act;
 
 int vit_abi_version(void);
@@ -34,7 +38,8 @@ const char* vit_last_error(void);
 /* ------------------------------------------------------------------------------------------------------------
  * GEMM with fused epilogue:  C[i][j] = epi( alpha * sum_r A(i,r) * B(j,r) )
  *   A(i,r) at a[i*lda + r] when a_kcontig, else a[r*lda + i]   (same for B with ldb / b_kcontig)
- *   epi(v): v += beta*C_old (f32 out only); v += bias[j]; act; v *= (aux(i,j) > 0) when aux;
+ *   epi(v): v += beta*C_old (f32 out only); v += bias[j]; act; v *= (aux(i,j) > 0) when aux (aux_dtype VIT_MASK4:
+ *           v *= aux bit);
  *           dropout(p, seed, index i*n + j) with 1/(1-p) scale; v += res(row(i), j) where row(i) = i % res_rowmod
  *           (res_rowmod == 0: i); stored at C[orow(i)*ldc + j], orow(i) = (i/G)*Gs + i%G when out_group_rows = G > 0.
  * Replaces: nn.Linear (transformer.py:12-18,38,56,58; vit.py:70,73), the conv-as-GEMM (vit.py:21-28), and all their
@@ -70,6 +75,9 @@ typedef struct vit_gemm_desc {
    * out_dtype rounding) — the bias gradient of the layer whose input gradient C is (transformer.py Linear backward),
    * finished by vit_colsum_finish.  Requires out_group_rows == 0. */
   float* colsum_part;
+  /* NULL, or a VIT_MASK4 buffer for C: the dropout keep bits when the epilogue applies dropout (transformer.py:47,59),
+   * else (C as stored > 0) — the ReLU-backward mask (transformer.py:57).  Requires out_group_rows == 0, split_k <= 1. */
+  void* mask_out;
 } vit_gemm_desc;
 
 /* Workspace vit_gemm can use: split_k > 1: the K-split fp32 slabs (required).  split_k <= 1: the slabs of the split-K

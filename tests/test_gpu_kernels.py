@@ -286,6 +286,57 @@ def test_gemm_split_k_tail(monkeypatch, variant):
         assert torch.equal(outs[1], (a.double() @ b.double().t()).float().bfloat16())
 
 
+def _mask4_pack(bits):
+    """bool [m, n] -> the VIT_MASK4 byte layout of include/vit_hip.h (byte ((i/4)*ceil(n/4) + j/4)*4 + i%4, bit j%4)."""
+    m, n = bits.shape
+    m4, n4 = -(-m // 4) * 4, -(-n // 4) * 4
+    b = torch.zeros(m4, n4, dtype=torch.int32, device=bits.device)
+    b[:m, :n] = bits.int()
+    b = b.view(m4 // 4, 4, n4 // 4, 4).permute(0, 2, 1, 3)
+    w = torch.tensor([1, 2, 4, 8], dtype=torch.int32, device=bits.device)
+    return (b * w).sum(-1).to(torch.uint8).reshape(-1)
+
+
+@pytest.mark.parametrize("variant", ["plain", "bias_relu", "bias_drop_res", "general", "tail", "f32_out", "ragged"])
+def test_gemm_mask4_produce_consume(monkeypatch, variant):
+    """mask_out = C's mask4 (C as stored > 0; dropout keep bits when the epilogue drops out), and a mask4 aux masks the
+    dgrad GEMM exactly as the bf16 tensor it was taken from (ReLU backward, transformer.py:57)."""
+    torch.manual_seed(13)
+    M, N, K = {"tail": (90 * 256 + 100, 768, 2304), "ragged": (1001, 776, 264)}.get(variant, (1000, 776, 256))
+    if variant == "general":
+        monkeypatch.setenv("VIT_GEMM_EPI_GENERAL", "1")
+    if variant == "tail":
+        monkeypatch.setenv("VIT_GEMM_TAIL", "1")
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    kw = {"bias_drop_res": dict(bias=bias, dropout_p=0.2, seed=3, res=res, ldres=N)}.get(
+        variant, dict(bias=bias, act=_ops.ACT_RELU) if variant != "plain" else {})
+    out = torch.empty(M, N, dtype=torch.float32 if variant == "f32_out" else torch.bfloat16, device=DEV)
+    mask = torch.full((_ops.mask4_bytes(M, N),), 0xAA, dtype=torch.uint8, device=DEV)
+    _ops.gemm(x, w, out, M, N, K, K, K, N, mask_out=mask, **kw)
+    if variant == "bias_drop_res":
+        from oracle.vit_oracle import dropout_keep
+        want = dropout_keep(3, (M, N), 0.2).to(DEV) > 0
+    else:
+        want = out > 0
+    assert torch.equal(mask, _mask4_pack(want))
+    # consumer: dgrad layout (B row-strided), mask4 aux == bf16 aux
+    if variant in ("plain", "bias_drop_res", "f32_out"):
+        return
+    g = torch.randn(M, K, device=DEV).bfloat16()
+    wt = (torch.randn(K, N, device=DEV) * 0.1).bfloat16()
+    d_ref = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    d_m = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    p_ref = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
+    p_m = torch.empty_like(p_ref)
+    _ops.gemm(g, wt, d_ref, M, N, K, K, N, N, b_kcontig=False, aux=out, ldaux=N, colsum_part=p_ref, alpha=1.25)
+    _ops.gemm(g, wt, d_m, M, N, K, K, N, N, b_kcontig=False, aux=mask, colsum_part=p_m, alpha=1.25)
+    assert torch.equal(d_m, d_ref)
+    assert torch.equal(p_m, p_ref)
+
+
 def _attn_ref(qkv, B, T, H, hd, scale):
     D = H * hd
     q, k, v = qkv.float().view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)

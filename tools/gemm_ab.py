@@ -19,7 +19,8 @@ M, D = 256 * 197, 768
 SHAPES = {  # name: m, n, k, a_kcontig, b_kcontig, epilogue
     "fwd_qkv": (M, 3 * D, D, True, True, None), "fwd_proj": (M, D, D, True, True, "bdr"),
     "fwd_fc1": (M, 4 * D, D, True, True, "bias_relu"), "fwd_fc2": (M, D, 4 * D, True, True, "bdr"),
-    "dgrad_fc2": (M, 4 * D, D, True, False, "aux"), "dgrad_fc1": (M, D, 4 * D, True, False, None),
+    "dgrad_fc2": (M, 4 * D, D, True, False, "aux"), "dgrad_fc2m": (M, 4 * D, D, True, False, "auxm"),
+    "fwd_fc1m": (M, 4 * D, D, True, True, "bias_relu_m"), "dgrad_fc1": (M, D, 4 * D, True, False, None),
     "dgrad_qkv": (M, D, 3 * D, True, False, None), "dgrad_proj": (M, D, D, True, False, None),
     "wgrad_fc1": (4 * D, D, M, False, False, "wgrad"), "wgrad_fc2": (D, 4 * D, M, False, False, "wgrad"),
     "wgrad_qkv": (3 * D, D, M, False, False, "wgrad"), "wgrad_proj": (D, D, M, False, False, "wgrad"),
@@ -37,7 +38,7 @@ def load(path):
     return lib
 
 
-def desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res):
+def desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res, mask):
     d = _lib.GemmDesc()
     d.a, d.b, d.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
     d.lda, d.ldb, d.ldc = a.stride(0), b.stride(0), n
@@ -46,10 +47,14 @@ def desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res):
     d.in_dtype = _lib.BF16
     d.out_dtype = _lib.F32 if epi == "wgrad" else _lib.BF16
     d.alpha, d.beta = 1.0, 0.0
-    if epi in ("bias_relu", "bdr"):
+    if epi in ("bias_relu", "bias_relu_m", "bdr"):
         d.bias = bias.data_ptr()
-    if epi == "bias_relu":
+    if epi in ("bias_relu", "bias_relu_m"):
         d.act = _lib.ACT_RELU
+    if epi == "bias_relu_m":
+        d.mask_out = mask.data_ptr()
+    if epi == "auxm":
+        d.aux, d.ldaux, d.aux_dtype = mask.data_ptr(), 0, _lib.MASK4
     if epi == "aux":
         d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), n, _lib.BF16
     if epi == "bdr":
@@ -83,6 +88,8 @@ def main():
         aux = (torch.rand(m, n, device="cuda", generator=g) - 0.3).bfloat16()
         res = torch.randn(m, n, device="cuda", generator=g).bfloat16()
         bias = torch.randn(n, device="cuda", generator=g)
+        mask = torch.randint(0, 256, (4 * ((m + 3) // 4) * ((n + 3) // 4),), device="cuda", generator=g,
+                             dtype=torch.uint8)
         c = torch.empty(m, n, dtype=torch.float32 if epi == "wgrad" else torch.bfloat16, device="cuda")
         split = libs[0].vit_gemm_split_k_hint(m, n, k, _lib.BF16) if epi == "wgrad" else 1
         times = {nm: [] for nm in names}
@@ -91,7 +98,7 @@ def main():
             for nm, lib, env in zip(names, libs, envs):
                 saved = {kk: os.environ.get(kk) for kk in env}
                 os.environ.update(env)
-                d = desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res)
+                d = desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res, mask)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 rc = lib.vit_gemm(ctypes.byref(d), stream)

@@ -15,6 +15,10 @@ for s in $STEPS; do
              --timeout-method thread > "$OUT/tests.log" 2>&1 ;;
     newtests) timeout -k 10 600 python -u -m pytest tests/test_gpu_dropin.py -v -m gpu -p no:cacheprovider \
              --timeout 300 --timeout-method thread > "$OUT/newtests.log" 2>&1 ;;
+    kern) timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -v -m gpu -p no:cacheprovider \
+             --timeout 120 --timeout-method thread > "$OUT/kern.log" 2>&1 ;;
+    ab) timeout -k 10 300 python -u tools/gemm_ab.py vision-transformer_amd/VisionTransformer/libvit_hip.so \
+          --shapes ${AB_SHAPES:-fwd_fc1,fwd_fc1m,dgrad_fc2,dgrad_fc2m} > "$OUT/ab.log" 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

@@ -422,8 +422,11 @@ class Engine:
             mk("ln_fwd", 0, 0.0, ln_b)
             a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
             mk("ln_fwd", 1)
-            mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 4 * M * D) * es)
-            h = _ops.linear(a2, self.ww[f"{l}.fc1_w"], bias=prm[f"{l}.fc1_b"], act=ACT_RELU)
+            # saved for the backward: the ReLU mask as 1 bit per element (mask4, read by fc2's dgrad epilogue instead
+            # of re-reading h: 1/16 of the bytes)
+            hm = _ops.mask4_empty(M, 4 * D, x.device) if save else None
+            mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 4 * M * D) * es + (M * D // 2 if save else 0))
+            h = _ops.linear(a2, self.ww[f"{l}.fc1_w"], bias=prm[f"{l}.fc1_b"], act=ACT_RELU, mask_out=hm)
             mk("gemm_fwd", 1)
             x_out = torch.empty(M, D, dtype=dt, device=x.device)
             mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (4 * M * D + 4 * D * D + 2 * M * D) * es)
@@ -431,7 +434,7 @@ class Engine:
                       res=x_mid, ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 1))
             mk("gemm_fwd", 1)
             if save:
-                blocks.append((x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h))
+                blocks.append((x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm))
             xcur = x_out
         # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
         z = torch.empty(B, D, dtype=torch.float32, device=x.device)
@@ -537,7 +540,7 @@ class Engine:
         for l in reversed(range(L)):
             if not need_from[l]:
                 break
-            x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h = tape.blocks[l]
+            x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm = tape.blocks[l]
             # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
             if req[f"{l}.fc2_w"]:
                 self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side, "gemm_wgrad", alpha=gs)
@@ -546,9 +549,9 @@ class Engine:
             dh = torch.empty(M, 4 * D, dtype=dt, device=dev)
             dh_part = torch.empty(_ops.colsum_part_rows(M), 4 * D, dtype=torch.float32, device=dev)
             # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
-            mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 8 * M * D) * es)
-            _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=h,
-                      ldaux=4 * D, colsum_part=dh_part, alpha=gs)
+            mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 4 * M * D) * es + M * D // 2)
+            _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
+                      colsum_part=dh_part, alpha=gs)
             mk("gemm_dgrad", 1)
             _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
             if req[f"{l}.fc1_w"]:

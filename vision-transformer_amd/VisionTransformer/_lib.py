@@ -10,9 +10,9 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
-F32, BF16 = 0, 1
+F32, BF16, MASK4 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
 
@@ -34,6 +34,7 @@ class GemmDesc(ctypes.Structure):
         ("out_group_rows", ctypes.c_int64), ("out_group_stride", ctypes.c_int64),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("colsum_part", ctypes.c_void_p),
+        ("mask_out", ctypes.c_void_p),
     ]
 
 

@@ -5,7 +5,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32  # noqa: F401
+from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, MASK4  # noqa: F401
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -33,12 +33,23 @@ def _need_cuda(*ts):
                                "the CPU restatement under oracle/ is test infrastructure, not a fallback")
 
 
+def mask4_bytes(m, n):
+    """Bytes of a VIT_MASK4 bit mask of an [m][n] tensor (include/vit_hip.h)."""
+    return 4 * ((m + 3) // 4) * ((n + 3) // 4)
+
+
+def mask4_empty(m, n, device):
+    return torch.empty(mask4_bytes(m, n), dtype=torch.uint8, device=device)
+
+
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=1.0, beta=0.0, bias=None,
          act=ACT_NONE, aux=None, ldaux=0, res=None, ldres=0, res_rowmod=0, dropout_p=0.0, seed=0, split_k=1,
-         out_group=(0, 0), workspace=None, colsum_part=None, stream=None):
+         out_group=(0, 0), workspace=None, colsum_part=None, mask_out=None, stream=None):
     """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  `colsum_part` (f32, colsum_part_rows(m) x n)
-    receives per-256-row-block column sums of C as stored — finish with colsum_finish.  Returns c."""
-    _need_cuda(a, b, c, bias, aux, res, colsum_part)
+    receives per-256-row-block column sums of C as stored — finish with colsum_finish.  `aux` may be a uint8 mask4
+    tensor (the ReLU mask saved by the forward); `mask_out` (uint8, mask4_bytes(m, n)) receives C's mask4 (dropout
+    keep bits when dropout_p > 0, else C > 0).  Returns c."""
+    _need_cuda(a, b, c, bias, aux, res, colsum_part, mask_out)
     if a.dtype != b.dtype:
         raise TypeError("gemm: A and B dtypes differ")
     if bias is not None and bias.dtype != torch.float32:
@@ -53,7 +64,16 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=
     d.bias = None if bias is None else bias.data_ptr()
     d.act = act
     if aux is not None:
-        d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), ldaux, dtype_code(aux)
+        if aux.dtype == torch.uint8:
+            if aux.numel() < mask4_bytes(m, n):
+                raise ValueError("gemm: mask4 aux too small")
+            d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), 0, MASK4
+        else:
+            d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), ldaux, dtype_code(aux)
+    if mask_out is not None:
+        if mask_out.dtype != torch.uint8 or mask_out.numel() < mask4_bytes(m, n):
+            raise ValueError("gemm: mask_out must be uint8 with >= mask4_bytes(m, n) elements")
+        d.mask_out = mask_out.data_ptr()
     if res is not None:
         d.res, d.ldres, d.res_rowmod, d.res_dtype = res.data_ptr(), ldres, res_rowmod, dtype_code(res)
     d.dropout_p, d.dropout_seed = dropout_p, seed & 0xFFFFFFFF

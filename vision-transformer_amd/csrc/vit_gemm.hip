@@ -37,7 +37,13 @@ struct EpiParams {
   int vec;  // all row strides/pointers allow 4-wide vector access
   float* csum;     // v4 fast epilogues: per-tile column sums of C as stored -> csum[tile row][n] (colsum_part)
   int64_t row0;    // global row of local row 0 (split-K tail launch): dropout indices use the global row
+  uint8_t* mask_out;  // mask4 of C: dropout keep bits, else (C as stored > 0) — see vit_hip.h
 };
+
+// mask4 layout of an [m][n] tensor: byte ((i/4) * ceil(n/4) + j/4) * 4 + i%4, bit j%4.  A row's 4-column group is
+// one byte and a 4-row x 4-column block one dword (byte = row), so a lane owning 4 columns of a row reads or writes a
+// byte, and over 4 consecutive rows a whole dword.
+VIT_DEV int64_t mask4_byte(int64_t i, int64_t j, int64_t n) { return (((i >> 2) * ((n + 3) >> 2)) + (j >> 2)) * 4 + (i & 3); }
 
 struct GemmArgs {
   const void* a;
@@ -84,17 +90,28 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
       for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
     }
     if (e.aux) {
-      float a[4];
-      if (e.aux_dtype == VIT_BF16) ld4<bf16_t>((const bf16_t*)e.aux + i * e.ldaux + j, a);
-      else ld4<float>((const float*)e.aux + i * e.ldaux + j, a);
+      if (e.aux_dtype == VIT_MASK4) {
+        const uint32_t bits = ((const uint8_t*)e.aux)[mask4_byte(i, j, e.n)];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
+        for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? v[r] : 0.f;
+      } else {
+        float a[4];
+        if (e.aux_dtype == VIT_BF16) ld4<bf16_t>((const bf16_t*)e.aux + i * e.ldaux + j, a);
+        else ld4<float>((const float*)e.aux + i * e.ldaux + j, a);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
+      }
     }
+    uint32_t keep = 0xfu;
     if (e.use_drop) {
       const uint32_t base = (uint32_t)((i + e.row0) * e.n + j);
+      keep = 0u;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        v[r] = vit_hash_u32(e.seed, base + r) >= e.drop_thr ? v[r] * e.drop_scale : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        const bool k = vit_hash_u32(e.seed, base + r) >= e.drop_thr;
+        keep |= (uint32_t)k << r;
+        v[r] = k ? v[r] * e.drop_scale : 0.f;
+      }
     }
     if (e.res) {
       float a[4];
@@ -104,7 +121,14 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
       for (int r = 0; r < 4; ++r) v[r] += a[r];
     }
     st4<TO>(cp, v);
+    if (e.mask_out) {
+      uint32_t bits = 0u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bits |= (uint32_t)(sizeof(TO) == 2 ? bf2f(f2bf(v[r])) > 0.f : v[r] > 0.f) << r;
+      e.mask_out[mask4_byte(i, j, e.n)] = (uint8_t)(e.use_drop ? keep : bits);
+    }
   } else {
+    uint32_t mbits = 0u;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t jj = j + r;
@@ -114,10 +138,23 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
       if (e.bias) x += e.bias[jj];
       if (e.act == VIT_ACT_RELU) x = fmaxf(x, 0.f);
       else if (e.act == VIT_ACT_GELU) x = gelu_erf(x);
-      if (e.aux) x = ld_any(e.aux, e.aux_dtype, i * e.ldaux + jj) > 0.f ? x : 0.f;
-      if (e.use_drop) x = vit_hash_u32(e.seed, (uint32_t)((i + e.row0) * e.n + jj)) >= e.drop_thr ? x * e.drop_scale : 0.f;
+      if (e.aux) {
+        const bool on = e.aux_dtype == VIT_MASK4 ? (((const uint8_t*)e.aux)[mask4_byte(i, jj, e.n)] >> (jj & 3)) & 1u
+                                                  : ld_any(e.aux, e.aux_dtype, i * e.ldaux + jj) > 0.f;
+        x = on ? x : 0.f;
+      }
+      bool k = true;
+      if (e.use_drop) {
+        k = vit_hash_u32(e.seed, (uint32_t)((i + e.row0) * e.n + jj)) >= e.drop_thr;
+        x = k ? x * e.drop_scale : 0.f;
+      }
       if (e.res) x += ld_any(e.res, e.res_dtype, rrow * e.ldres + jj);
       st1<TO>(cp + r, x);
+      const float stored = ld1<TO>(cp + r);
+      mbits |= (uint32_t)(e.use_drop ? k : stored > 0.f) << ((jj & 3));
+    }
+    if (e.mask_out) {                                   // j % 4 == 0 here: the row's 4-column group is one byte
+      e.mask_out[mask4_byte(i, j, e.n)] = (uint8_t)mbits;
     }
   }
 }
@@ -487,7 +524,8 @@ enum EpiKind : int {
   EPI_AUX = 2,        // alpha * acc masked by aux > 0 (ReLU backward)
   EPI_BDR = 3,        // dropout(alpha * acc [+ bias]) [+ res]
   EPI_SLAB = 4,       // split-K fp32 slab
-  EPI_GENERAL = 5     // epilogue4 (beta, row groups, row-modulo residual, unaligned, any combination)
+  EPI_GENERAL = 5,    // epilogue4 (beta, row groups, row-modulo residual, unaligned, any combination)
+  EPI_AUXM = 6        // alpha * acc masked by a mask4 bit (ReLU backward from the forward's stored mask)
 };
 
 // Kinds whose row epilogue reads a second [m][n]-shaped bf16 operand (ReLU mask / residual).  Those reads are
@@ -496,12 +534,16 @@ enum EpiKind : int {
 // every store issued before it (one vmcnt counter).
 template <int KIND>
 VIT_DEV bool v4_has_pre(const EpiParams& e) {
-  return KIND == EPI_AUX || (KIND == EPI_BDR && e.res != nullptr);
+  return KIND == EPI_AUX || KIND == EPI_AUXM || (KIND == EPI_BDR && e.res != nullptr);
 }
 
 template <int KIND>
 VIT_DEV uint2 v4_pre_load(const EpiParams& e, int64_t i, int64_t j) {
   uint2 r = make_uint2(0u, 0u);
+  if (KIND == EPI_AUXM) {                          // i % 4 == 0: the dword of rows i..i+3 (row groups are allocated whole)
+    if (i < e.m && j < e.n) r.x = *reinterpret_cast<const uint32_t*>((const uint8_t*)e.aux + mask4_byte(i, j, e.n));
+    return r;
+  }
   if (i < e.m && j < e.n) {
     const bf16_t* p = KIND == EPI_AUX ? (const bf16_t*)e.aux + i * e.ldaux + j : (const bf16_t*)e.res + i * e.ldres + j;
     r = *reinterpret_cast<const uint2*>(p);
@@ -516,18 +558,20 @@ VIT_DEV void unpack_bf16x4(uint2 u, float (&a)[4]) {
   a[3] = __uint_as_float(u.y & 0xffff0000u);
 }
 
+// Returns the row's mask4 nibble (dropout keep bits for EPI_BDR with dropout, else stored value > 0) for the fast
+// kinds that produce one (the caller stores 4 rows' nibbles as one dword); 0 otherwise.
 template <class TO, int KIND>
-VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_t j, const float (&b4)[4], bool relu,
-                        bool gelu, float v[4], uint2 pre = make_uint2(0u, 0u)) {
+VIT_DEV uint32_t v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_t j, const float (&b4)[4],
+                            bool relu, bool gelu, float v[4], uint2 pre = make_uint2(0u, 0u)) {
   if (KIND == EPI_GENERAL) {
     epilogue4<TO>(e, i, j, v);
-    return;
+    return 0u;
   }
   if (KIND == EPI_SLAB) {
     slab_store4(g.ws, g.M, g.N, i, j, v);          // g.ws: this workgroup's K-slice slab (set by the kernel)
-    return;
+    return 0u;
   }
-  if (i >= e.m || j >= e.n) return;                 // fast kinds: n % 4 == 0 and 16-B aligned rows (e.vec)
+  if (i >= e.m || j >= e.n) return 0u;              // fast kinds: n % 4 == 0 and 16-B aligned rows (e.vec)
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] *= e.alpha;
   if (KIND == EPI_BIAS_ACT || KIND == EPI_BDR) {
@@ -549,11 +593,20 @@ VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
   }
+  if (KIND == EPI_AUXM) {                           // pre.x = this row's mask4 nibble
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (pre.x >> r) & 1u ? v[r] : 0.f;
+  }
+  uint32_t keep = 0u;
   if (KIND == EPI_BDR) {
     if (e.use_drop) {
       const uint32_t base = (uint32_t)((i + e.row0) * e.n + j);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = vit_hash_u32(e.seed, base + r) >= e.drop_thr ? v[r] * e.drop_scale : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        const bool k = vit_hash_u32(e.seed, base + r) >= e.drop_thr;
+        keep |= (uint32_t)k << r;
+        v[r] = k ? v[r] * e.drop_scale : 0.f;
+      }
     }
     if (e.res) {                                     // res is bf16 (host-checked), prefetched
       float a[4];
@@ -563,6 +616,11 @@ VIT_DEV void v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_
     }
   }
   st4<TO>((TO*)e.c + i * e.ldc + j, v);
+  if (KIND == EPI_BDR && e.use_drop) return keep;
+  uint32_t pos = 0u;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) pos |= (uint32_t)(sizeof(TO) == 2 ? bf2f(f2bf(v[r])) > 0.f : v[r] > 0.f) << r;
+  return pos;
 }
 
 template <bool KC>
@@ -714,8 +772,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   const int64_t nkt = g.K / BK;
   const int64_t kt0 = sidx * g.kt_per_split;
   const int nk = (int)max((int64_t)0, min(nkt, kt0 + g.kt_per_split) - kt0);
+#ifndef V4_GLDS
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
+#endif
   const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
   const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
   uint32_t oa0[2], oa1[2], ob0[2], ob1[2];
@@ -873,14 +933,22 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   uint2 pre[2][16];
   const bool has_pre = v4_has_pre<KIND>(e);
   // fused column sums of C as stored (the bias gradient of the Linear whose input gradient C is)
-  const bool cs_on = (KIND == EPI_PLAIN || KIND == EPI_BIAS_ACT || KIND == EPI_AUX || KIND == EPI_BDR) &&
-                     e.csum != nullptr;
+  const bool cs_on = (KIND == EPI_PLAIN || KIND == EPI_BIAS_ACT || KIND == EPI_AUX || KIND == EPI_AUXM ||
+                      KIND == EPI_BDR) && e.csum != nullptr;
+  // mask4 of C: 4 rows' nibbles of this lane's column group -> one dword store per 4 rows (EPI_GENERAL writes it in
+  // epilogue4, the split-K reduce after EPI_SLAB)
+  const bool mk_on = KIND != EPI_GENERAL && KIND != EPI_SLAB && e.mask_out != nullptr;
+  uint32_t mword = 0u;
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
   if (has_pre) {
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
+      for (int rr = 0; rr < 16; ++rr) {
+        if (KIND != EPI_AUXM) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
+        else if ((rr & 3) == 0) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
+        else pre[mh][rr] = make_uint2(pre[mh][rr & ~3].x >> (8 * (rr & 3)), 0u);
+      }
   }
   __syncthreads();                                        // every wave's k-loop LDS reads are done, no DMA pending
 #pragma unroll
@@ -905,7 +973,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 #ifdef VIT_GEMM_NOEPI
       if (v[0] != 1234.5f) continue;
 #endif
-      v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
+      const uint32_t nib = v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
+      if (mk_on) {
+        mword |= (nib & 0xfu) << (8 * (rr & 3));
+        if ((rr & 3) == 3) {                            // rows i-3..i: one dword (row groups are allocated whole)
+          if (i - 3 < e.m && j < e.n)
+            *reinterpret_cast<uint32_t*>(e.mask_out + mask4_byte(i - 3, j, e.n)) = mword;
+          mword = 0u;
+        }
+      }
       if (cs_on && i < e.m) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[r] += sizeof(TO) == 2 ? bf2f(f2bf(v[r])) : v[r];
@@ -1088,6 +1164,11 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
   VIT_REQUIRE(d->in_dtype == VIT_F32 || d->in_dtype == VIT_BF16, "vit_gemm: bad in_dtype %d", d->in_dtype);
   VIT_REQUIRE(d->out_dtype == VIT_F32 || d->out_dtype == VIT_BF16, "vit_gemm: bad out_dtype %d", d->out_dtype);
   VIT_REQUIRE(d->beta == 0.f || d->out_dtype == VIT_F32, "vit_gemm: beta requires f32 output");
+  VIT_REQUIRE(!d->aux || d->aux_dtype == VIT_F32 || d->aux_dtype == VIT_BF16 || d->aux_dtype == VIT_MASK4,
+              "vit_gemm: bad aux_dtype %d", d->aux_dtype);
+  VIT_REQUIRE(!d->mask_out || d->out_group_rows == 0, "vit_gemm: mask_out needs ungrouped output rows");
+  VIT_REQUIRE(!d->mask_out || aligned(d->mask_out, 4), "vit_gemm: mask_out must be 4-B aligned");
+  VIT_REQUIRE(!d->aux || d->aux_dtype != VIT_MASK4 || aligned(d->aux, 4), "vit_gemm: mask4 aux must be 4-B aligned");
   VIT_REQUIRE(d->dropout_p >= 0.f && d->dropout_p < 1.f, "vit_gemm: dropout_p out of range");
   const int split = d->split_k > 1 ? d->split_k : 1;
 
@@ -1108,9 +1189,10 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
   e.grp_stride = d->out_group_stride;
   e.csum = nullptr;
   e.row0 = row0;
+  e.mask_out = (uint8_t*)d->mask_out;
   bool cs_fused = false;
   e.vec = (d->n % 4 == 0) && (d->ldc % 4 == 0) && aligned(d->c, 16) && aligned(d->bias, 16) &&
-          (!d->aux || (d->ldaux % 4 == 0 && aligned(d->aux, 16))) &&
+          (!d->aux || d->aux_dtype == VIT_MASK4 || (d->ldaux % 4 == 0 && aligned(d->aux, 16))) &&
           (!d->res || (d->ldres % 4 == 0 && aligned(d->res, 16)));
 
   GemmArgs g{};
@@ -1165,6 +1247,8 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     else if (fast && e.bias && !e.aux && !e.use_drop && !e.res) kind = EPI_BIAS_ACT;
     else if (fast && e.aux && e.aux_dtype == VIT_BF16 && !e.bias && e.act == VIT_ACT_NONE && !e.use_drop && !e.res)
       kind = EPI_AUX;
+    else if (fast && e.aux && e.aux_dtype == VIT_MASK4 && !e.bias && e.act == VIT_ACT_NONE && !e.use_drop && !e.res)
+      kind = EPI_AUXM;
     else if (fast && !e.aux && e.act == VIT_ACT_NONE && (e.use_drop || e.res) && (!e.res || e.res_dtype == VIT_BF16))
       kind = EPI_BDR;
     const char* dk = getenv("VIT_GEMM_EPI_GENERAL");      // A/B switch: force the general epilogue
@@ -1175,6 +1259,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     else if (out_bf && kind == EPI_PLAIN) launched = EPI_PLAIN;
     else if (out_bf && akc && bkc && (kind == EPI_BIAS_ACT || kind == EPI_BDR)) launched = kind;
     else if (out_bf && akc && !bkc && kind == EPI_AUX) launched = EPI_AUX;
+    else if (out_bf && akc && !bkc && kind == EPI_AUXM) launched = EPI_AUXM;
     cs_fused = v4 && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
     e.csum = cs_fused ? d->colsum_part : nullptr;
 #define V4(AK, BKK, TO, KIND) gemm_bf16_v4<AK, BKK, TO, KIND><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes)
@@ -1187,6 +1272,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
       else if (AK && BKK && launched == EPI_BIAS_ACT) V4(AK, BKK, bf16_t, EPI_BIAS_ACT);                       \
       else if (AK && BKK && launched == EPI_BDR) V4(AK, BKK, bf16_t, EPI_BDR);                                 \
       else if (AK && !BKK && launched == EPI_AUX) V4(AK, BKK, bf16_t, EPI_AUX);                                \
+      else if (AK && !BKK && launched == EPI_AUXM) V4(AK, BKK, bf16_t, EPI_AUXM);                              \
       else V4(AK, BKK, bf16_t, EPI_GENERAL);                                                                   \
     } else if (v2) {                                                                                           \
       if (out_bf && split == 1) gemm_bf16_v2<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);     \
@@ -1248,7 +1334,9 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     vit_gemm_desc dt = *d;
     dt.a = (const char*)d->a + (d->a_kcontig ? r * d->lda : r) * 2;
     dt.c = (char*)d->c + r * d->ldc * esz(d->out_dtype);
-    if (d->aux) dt.aux = (const char*)d->aux + r * d->ldaux * esz(d->aux_dtype);
+    const int64_t mask_off = (r / 4) * ((d->n + 3) / 4) * 4;   // r % 256 == 0: whole mask4 row groups
+    if (d->aux) dt.aux = (const char*)d->aux + (d->aux_dtype == VIT_MASK4 ? mask_off : r * d->ldaux * esz(d->aux_dtype));
+    if (d->mask_out) dt.mask_out = (char*)d->mask_out + mask_off;
     if (d->res) dt.res = (const char*)d->res + r * d->ldres * esz(d->res_dtype);
     if (d->colsum_part) dt.colsum_part = d->colsum_part + (r / 256) * d->n;
     dt.m = d->m - r;
