@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 6
+#define VIT_ABI_VERSION 7
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -76,8 +76,11 @@ typedef struct vit_gemm_desc {
    * finished by vit_colsum_finish.  Requires out_group_rows == 0. */
   float* colsum_part;
   /* NULL, or a VIT_MASK4 buffer for C: the dropout keep bits when the epilogue applies dropout (transformer.py:47,59),
-   * else (C as stored > 0) — the ReLU-backward mask (transformer.py:57).  Requires out_group_rows == 0, split_k <= 1. */
+   * else (C as stored > 0) — the ReLU-backward mask (transformer.py:57).  Requires out_group_rows == 0. */
   void* mask_out;
+  /* 0/1, or S: the dropout index of output row i is (i * S) * n + j — C computes rows i*S of a larger [m*S][n] tensor
+   * (the last block's token-0 rows, ldA = S*K), and its dropout draws the same bits as the full tensor's rows. */
+  int64_t dropout_row_stride;
 } vit_gemm_desc;
 
 /* Workspace vit_gemm can use: split_k > 1: the K-split fp32 slabs (required).  split_k <= 1: the slabs of the split-K
@@ -112,7 +115,9 @@ int vit_embed_cls(const float* cls, const float* pos, void* x0, int32_t dtype, i
  *   bwd: dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma;
  *        dx_out = dx (+ dres when dres != NULL)                    — fused residual-gradient add (transformer.py:77-78)
  *        drop_out = dx_out * keep(drop_seed, i*cols + j)            — fused dropout backward of the producer branch,
- *                   WITHOUT the 1/(1-p) scale (exact in bf16: the consumers apply it, e.g. as GEMM alpha)
+ *                   WITHOUT the 1/(1-p) scale (exact in bf16: the consumers apply it, e.g. as GEMM alpha); with
+ *                   drop_mask (VIT_MASK4 [rows][cols], the producing GEMM's mask_out) the keep bits are read from it
+ *                   instead of re-hashed
  *        dgamma/dbeta: per-workgroup partials in `partial` [2][nparts][cols], reduced by vit_colsum_finish
  *        (deterministic); with `osum` != 0 also partial [2] = column sums of the stored gradient output (drop_out
  *        / (1-p) when drop_out is given, else dx_out) — the bias gradient of the Linear that consumes it, so
@@ -123,8 +128,8 @@ int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma, const floa
 int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols);
 int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
                       const float* mean, const float* rstd, const void* dres, void* dx_out, void* drop_out,
-                      float drop_p, uint32_t drop_seed, float* partial, int32_t osum, int64_t rows, int64_t cols,
-                      int32_t dtype, void* stream);
+                      float drop_p, uint32_t drop_seed, const void* drop_mask, float* partial, int32_t osum,
+                      int64_t rows, int64_t cols, int32_t dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------
  * Multi-head self-attention (transformer.py:9-31 per head, :44-45 concat): qkv[B*T][3*D] with Q at columns
@@ -171,6 +176,10 @@ int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n, float p, u
                     void* stream);
 /* dx = dy * (y > 0): ReLU backward for the module-level FeedForward path (transformer.py:57). */
 int vit_relu_bwd(const void* dy, const void* y, void* dx, int32_t dtype, int64_t n, void* stream);
+/* y[i][j] = x[i][j] * bit(mask, i, j) * scale — a dropout backward from the forward's saved VIT_MASK4 keep bits
+ * (transformer.py:59 backward at the head, where the gradient covers the token-0 rows only). */
+int vit_mask4_apply(const void* x, int64_t ldx, int32_t x_dtype, void* y, int64_t ldy, int32_t y_dtype,
+                    const void* mask, int64_t rows, int64_t cols, float scale, void* stream);
 int vit_gelu_fwd(const float* x, float* y, int64_t n, void* stream);
 int vit_gelu_bwd(const float* x, const float* dy, float* dx, int64_t n, void* stream);
 int vit_softmax_xent(const float* logits, const int64_t* labels, int64_t rows, int64_t classes, float* loss,

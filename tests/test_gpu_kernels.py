@@ -321,7 +321,11 @@ def test_gemm_mask4_produce_consume(monkeypatch, variant):
         want = dropout_keep(3, (M, N), 0.2).to(DEV) > 0
     else:
         want = out > 0
-    assert torch.equal(mask, _mask4_pack(want))
+    # bytes of rows >= M (padding of the last 4-row group) are unspecified
+    nq = -(-N // 4)
+    b = torch.arange(mask.numel(), device=DEV)
+    valid = (b // 4 // nq) * 4 + b % 4 < M
+    assert torch.equal(mask[valid], _mask4_pack(want)[valid])
     # consumer: dgrad layout (B row-strided), mask4 aux == bf16 aux
     if variant in ("plain", "bias_drop_res", "f32_out"):
         return

@@ -19,6 +19,9 @@ for s in $STEPS; do
              --timeout 120 --timeout-method thread > "$OUT/kern.log" 2>&1 ;;
     ab) timeout -k 10 300 python -u tools/gemm_ab.py vision-transformer_amd/VisionTransformer/libvit_hip.so \
           --shapes ${AB_SHAPES:-fwd_fc1,fwd_fc1m,dgrad_fc2,dgrad_fc2m} > "$OUT/ab.log" 2>&1 ;;
+    model) timeout -k 10 900 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_dropin.py -x -v -m gpu \
+             -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/model.log" 2>&1 ;;
+    ln) timeout -k 10 300 python -u tools/ln_bench.py > "$OUT/ln.log" 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

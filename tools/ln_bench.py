@@ -41,6 +41,12 @@ def main():
     t = timeit(lambda: _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, drop_out=drop, drop_p=0.2,
                                           drop_seed=1, partial=part, osum=True), args.reps)
     print(f"ln bwd (+osum)      {t:7.1f} us  {5 * rows * cols * 2 / t / 1e6:6.2f} TB/s")
+    mask = torch.randint(0, 256, (_ops.mask4_bytes(rows, cols),), dtype=torch.uint8, device="cuda")
+    t = timeit(lambda: _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, drop_out=drop, drop_p=0.2,
+                                          drop_mask=mask, partial=part, osum=True), args.reps)
+    print(f"ln bwd (+osum,mask) {t:7.1f} us  {5 * rows * cols * 2 / t / 1e6:6.2f} TB/s")
+    t = timeit(lambda: _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, partial=part, osum=True), args.reps)
+    print(f"ln bwd (no drop)    {t:7.1f} us  {4 * rows * cols * 2 / t / 1e6:6.2f} TB/s")
     t = timeit(lambda: _ops.colsum_finish(part, outs), args.reps)
     print(f"colsum_finish x3    {t:7.1f} us")
 

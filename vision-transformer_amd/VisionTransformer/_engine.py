@@ -88,7 +88,7 @@ def head_split_for(m, n, k):
 class Tape:
     """Activations saved by a training forward."""
     __slots__ = ("B", "cols", "blocks", "z", "u", "gz", "zn", "mh", "rh", "seed", "training", "x_shape", "x_dtype",
-                 "x_grad")
+                 "x_grad", "pruned")
 
 
 class Engine:
@@ -320,6 +320,14 @@ class Engine:
         for t in (dy, x) if ws is None else (dy, x, ws):
             t.record_stream(side)          # the caching allocator must not hand these out before `side` is done
 
+    def _gemm_rows(self, pr, a, b, c, m, n, k, lda, ldb, ldc, **kw):
+        """A token-row GEMM; `pr` (the pruned last block, m = B rows): split-K over the otherwise idle CUs — a few
+        256x256 tiles would each run one long k-loop on one CU."""
+        split = split_k_for(m, n, k, a.dtype) if pr else 1
+        if split > 1:
+            kw.update(split_k=split, workspace=self._workspace(split * m * n * 4))
+        return _ops.gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw)
+
     def _head_gemm(self, a, b, c, m, n, k, lda, ldb, ldc, **kw):
         split = head_split_for(m, n, k)
         ws = self._workspace(split * m * n * 4) if split > 1 else None
@@ -394,6 +402,13 @@ class Engine:
         mk("gemm_fwd", 1)
         _ops.embed_cls(prm["cls"], prm["pos"], xcur, B, T, D)                           # CLS appended LAST (vit.py:41)
         blocks = []
+        # The classifier reads token 0 of the last block's output only (vit.py:80), and everything after the last
+        # attention is per token: the last block's proj / LN2 / MLP (and their backward) run on the B token-0 rows
+        # (rows b*T, row stride T*D; dropout bits drawn at the full tensor's indices) — the same logits, loss and
+        # gradients as computing all B*T rows and discarding the rest.  VIT_PRUNE_LAST=0 computes every row.
+        prune = os.environ.get("VIT_PRUNE_LAST", "1") != "0"
+        drop_p = DROPOUT_P if training else 0.0
+        keep_masks = save and training          # the backward reads the forward's dropout keep bits (mask4)
         for l in range(L):
             blk = model.transformer_encoder.blocks[l]
             x_in = xcur
@@ -414,31 +429,40 @@ class Engine:
             o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
             mk("attn_fwd", 1)
             blk.multi_head.attention_probs = probs
-            x_mid = torch.empty(M, D, dtype=dt, device=x.device)
-            mk("gemm_fwd", 0, 2.0 * M * D * D, (3 * M * D + D * D) * es)
-            _ops.gemm(o, self.ww[f"{l}.proj_w"], x_mid, M, D, D, D, D, D, bias=prm[f"{l}.proj_b"], res=x_in,
-                      ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 0))
+            # rows of the post-attention part: all M, or (last block, pruned) the B token-0 rows b*T
+            pr = prune and l == L - 1
+            R, rs = (B, T) if pr else (M, 1)
+            pm = _ops.mask4_empty(R, D, x.device) if keep_masks else None      # proj dropout keep bits
+            fm = _ops.mask4_empty(R, D, x.device) if keep_masks else None      # fc2 dropout keep bits
+            x_mid = torch.empty(R, D, dtype=dt, device=x.device)
+            mk("gemm_fwd", 0, 2.0 * R * D * D, (3 * R * D + D * D) * es)
+            self._gemm_rows(pr, o, self.ww[f"{l}.proj_w"], x_mid, R, D, D, rs * D, D, D, bias=prm[f"{l}.proj_b"],
+                            res=x_in, ldres=rs * D, dropout_p=drop_p, seed=site_seed(seed, l, 0),
+                            drop_row_stride=rs, mask_out=pm)
             mk("gemm_fwd", 1)
-            mk("ln_fwd", 0, 0.0, ln_b)
+            mk("ln_fwd", 0, 0.0, 2 * R * D * es + 8 * R)
             a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
             mk("ln_fwd", 1)
             # saved for the backward: the ReLU mask as 1 bit per element (mask4, read by fc2's dgrad epilogue instead
             # of re-reading h: 1/16 of the bytes)
-            hm = _ops.mask4_empty(M, 4 * D, x.device) if save else None
-            mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 4 * M * D) * es + (M * D // 2 if save else 0))
-            h = _ops.linear(a2, self.ww[f"{l}.fc1_w"], bias=prm[f"{l}.fc1_b"], act=ACT_RELU, mask_out=hm)
+            hm = _ops.mask4_empty(R, 4 * D, x.device) if save else None
+            mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + (R * D // 2 if save else 0))
+            h = torch.empty(R, 4 * D, dtype=dt, device=x.device)
+            self._gemm_rows(pr, a2, self.ww[f"{l}.fc1_w"], h, R, 4 * D, D, D, D, 4 * D, bias=prm[f"{l}.fc1_b"],
+                            act=ACT_RELU, mask_out=hm)
             mk("gemm_fwd", 1)
-            x_out = torch.empty(M, D, dtype=dt, device=x.device)
-            mk("gemm_fwd", 0, 2.0 * M * 4 * D * D, (4 * M * D + 4 * D * D + 2 * M * D) * es)
-            _ops.gemm(h, self.ww[f"{l}.fc2_w"], x_out, M, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
-                      res=x_mid, ldres=D, dropout_p=DROPOUT_P if training else 0.0, seed=site_seed(seed, l, 1))
+            x_out = torch.empty(R, D, dtype=dt, device=x.device)
+            mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + 2 * R * D) * es)
+            self._gemm_rows(pr, h, self.ww[f"{l}.fc2_w"], x_out, R, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
+                            res=x_mid, ldres=D, dropout_p=drop_p, seed=site_seed(seed, l, 1), drop_row_stride=rs,
+                            mask_out=fm)
             mk("gemm_fwd", 1)
             if save:
-                blocks.append((x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm))
+                blocks.append((x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm))
             xcur = x_out
         # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
         z = torch.empty(B, D, dtype=torch.float32, device=x.device)
-        _ops.copy2d(xcur, T * D, z, D, B, D)
+        _ops.copy2d(xcur, D if prune else T * D, z, D, B, D)
         u = self._head_linear(z, prm["h0_w"], prm["h0_b"])
         gz = _ops.gelu_fwd(u)
         zn, mh, rh = _ops.layernorm_fwd(gz, prm["hln_w"], prm["hln_b"], eps=LN_EPS)
@@ -447,7 +471,7 @@ class Engine:
             tape.B, tape.cols, tape.blocks = B, cols, blocks
             tape.x_shape, tape.x_dtype = tuple(x.shape), x.dtype
             tape.z, tape.u, tape.gz, tape.zn, tape.mh, tape.rh = z, u, gz, zn, mh, rh
-            tape.seed, tape.training = seed, training
+            tape.seed, tape.training, tape.pruned = seed, training, prune
         return logits, tape
 
     # ------------------------------------------------------------------------------------------------------------
@@ -524,15 +548,18 @@ class Engine:
         if not need_from[L - 1]:
             self._finish_buckets()
             return None
-        # ---- d(encoder output): only token-0 rows are nonzero
-        dx = torch.zeros(M, D, dtype=dt, device=dev)
-        _ops.copy2d(dz, D, dx, T * D, B, D)
+        # ---- d(encoder output): only token-0 rows are nonzero.  Pruned (see forward): the last block's FFN / proj
+        # backward runs on those B rows; otherwise on all M rows, zero outside them.
+        pruned = tape.pruned
+        R0 = B if pruned else M
+        dx = (torch.empty if pruned else torch.zeros)(R0, D, dtype=dt, device=dev)
+        _ops.copy2d(dz, D, dx, D if pruned else T * D, B, D)
         # Dropout backward as a bare mask (exact in bf16); its 1/(1-p) goes into every consumer of the masked gradient
-        # (GEMM alpha, column-sum alpha, the LN kernels' bias-gradient sums) instead of a rounding of its own.
+        # (GEMM alpha, column-sum alpha, the LN kernels' bias-gradient sums) instead of a rounding of its own.  The
+        # keep bits are the ones the forward's GEMM epilogues saved (mask4), not a re-hash.
         gs = 1.0 / (1.0 - DROPOUT_P) if tape.training else 1.0
-        g1 = torch.empty_like(dx)
         if tape.training:
-            _ops.dropout_bwd(dx, g1, DROPOUT_P, site_seed(tape.seed, L - 1, 1), scale=1.0)
+            g1 = _ops.mask4_apply(dx, torch.empty_like(dx), tape.blocks[L - 1][15], 1.0)
         else:
             g1 = dx
         side = self._side_stream()
@@ -540,44 +567,53 @@ class Engine:
         for l in reversed(range(L)):
             if not need_from[l]:
                 break
-            x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm = tape.blocks[l]
+            x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm = tape.blocks[l]
+            pr = pruned and l == L - 1
+            R, rs = (B, T) if pr else (M, 1)
             # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
             if req[f"{l}.fc2_w"]:
-                self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, M, D, 4 * D, beta, side, "gemm_wgrad", alpha=gs)
+                self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, R, D, 4 * D, beta, side, "gemm_wgrad", alpha=gs)
             if not g1_summed:
-                self._colsum(g1, M, D, D, gw[f"{l}.fc2_b"], beta, alpha=gs)
-            dh = torch.empty(M, 4 * D, dtype=dt, device=dev)
-            dh_part = torch.empty(_ops.colsum_part_rows(M), 4 * D, dtype=torch.float32, device=dev)
+                self._colsum(g1, R, D, D, gw[f"{l}.fc2_b"], beta, alpha=gs)
+            dh = torch.empty(R, 4 * D, dtype=dt, device=dev)
+            dh_part = torch.empty(_ops.colsum_part_rows(R), 4 * D, dtype=torch.float32, device=dev)
             # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
-            mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (M * D + 4 * D * D + 4 * M * D) * es + M * D // 2)
-            _ops.gemm(g1, self.ww[f"{l}.fc2_w"], dh, M, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
-                      colsum_part=dh_part, alpha=gs)
+            mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + R * D // 2)
+            self._gemm_rows(pr, g1, self.ww[f"{l}.fc2_w"], dh, R, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
+                            colsum_part=dh_part, alpha=gs)
             mk("gemm_dgrad", 1)
             _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
             if req[f"{l}.fc1_w"]:
-                self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, M, 4 * D, D, beta, side, "gemm_wgrad")
-            da2 = torch.empty(M, D, dtype=dt, device=dev)
-            mk("gemm_dgrad", 0, 2.0 * M * 4 * D * D, (4 * M * D + 4 * D * D + M * D) * es)
-            _ops.gemm(dh, self.ww[f"{l}.fc1_w"], da2, M, D, 4 * D, 4 * D, D, D, b_kcontig=False)
+                self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, R, 4 * D, D, beta, side, "gemm_wgrad")
+            da2 = torch.empty(R, D, dtype=dt, device=dev)
+            mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + R * D) * es)
+            self._gemm_rows(pr, dh, self.ww[f"{l}.fc1_w"], da2, R, D, 4 * D, 4 * D, D, D, b_kcontig=False)
             mk("gemm_dgrad", 1)
-            dx_mid = torch.empty(M, D, dtype=dt, device=dev)
-            g0 = torch.empty(M, D, dtype=dt, device=dev) if tape.training else None
+            dx_mid = torch.empty(R, D, dtype=dt, device=dev)
+            g0 = torch.empty(R, D, dtype=dt, device=dev) if tape.training else None
             # ln2 backward + residual add + dropout backward of the MHA branch; its third partial set is the column
             # sums of g0 as stored = the proj bias gradient
-            mk("ln_bwd", 0, 0.0, (3 + 1 + (g0 is not None)) * M * D * es + 8 * M)
-            part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx,
-                                      drop_out=g0, drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l, 0), osum=True)
+            mk("ln_bwd", 0, 0.0, (3 + 1 + (g0 is not None)) * R * D * es + 8 * R + R * D // 8)
+            part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx, drop_out=g0,
+                                      drop_p=DROPOUT_P, drop_mask=pm, osum=True)
             mk("ln_bwd", 1)
             _ops.colsum_finish(part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta=beta)
             if g0 is None:
                 g0 = dx_mid
             # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
             if req[f"{l}.proj_w"]:
-                self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, M, D, D, beta, side, "gemm_wgrad", alpha=gs)
-            do = torch.empty(M, D, dtype=dt, device=dev)
-            mk("gemm_dgrad", 0, 2.0 * M * D * D, (2 * M * D + D * D) * es)
-            _ops.gemm(g0, self.ww[f"{l}.proj_w"], do, M, D, D, D, D, D, b_kcontig=False, alpha=gs)
+                self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, R, D, rs * D, beta, side, "gemm_wgrad", alpha=gs)
+            do = torch.empty(R, D, dtype=dt, device=dev)
+            mk("gemm_dgrad", 0, 2.0 * R * D * D, (2 * R * D + D * D) * es)
+            self._gemm_rows(pr, g0, self.ww[f"{l}.proj_w"], do, R, D, D, D, D, D, b_kcontig=False, alpha=gs)
             mk("gemm_dgrad", 1)
+            if pr:
+                # back to all M rows for the attention backward (zero outside the token-0 rows)
+                do_full = torch.zeros(M, D, dtype=dt, device=dev)
+                _ops.copy2d(do, D, do_full, T * D, B, D)
+                dxm_full = torch.zeros(M, D, dtype=dt, device=dev)
+                _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
+                do, dx_mid = do_full, dxm_full
             mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 8 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                           else 0))
             dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
@@ -595,7 +631,7 @@ class Engine:
             # = the fc2 bias gradient of block l-1
             mk("ln_bwd", 0, 0.0, (3 + 1 + (g1n is not None)) * M * D * es + 8 * M)
             part = _ops.layernorm_bwd(da1, x_in, prm[f"{l}.ln1_w"], m1, r1, dx_in, dres=dx_mid, drop_out=g1n,
-                                      drop_p=DROPOUT_P, drop_seed=site_seed(tape.seed, l - 1, 1) if l > 0 else 0,
+                                      drop_p=DROPOUT_P, drop_mask=tape.blocks[l - 1][15] if g1n is not None else None,
                                       osum=l > 0)
             mk("ln_bwd", 1)
             outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if l > 0 else [])

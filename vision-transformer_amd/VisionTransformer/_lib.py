@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 F32, BF16, MASK4 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
@@ -35,6 +35,7 @@ class GemmDesc(ctypes.Structure):
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("colsum_part", ctypes.c_void_p),
         ("mask_out", ctypes.c_void_p),
+        ("dropout_row_stride", ctypes.c_int64),
     ]
 
 
@@ -57,7 +58,7 @@ _SIGS = {
     "vit_embed_cls": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _I64, _I64, _P]),
     "vit_layernorm_fwd": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _I64, _I64, _F, _I32, _P]),
     "vit_layernorm_bwd_parts": (_I64, [_I64, _I64]),
-    "vit_layernorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _F, _U32, _P, _I32, _I64,
+    "vit_layernorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _F, _U32, _P, _P, _I32, _I64,
                                          _I64, _I32, _P]),
     "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
@@ -67,6 +68,7 @@ _SIGS = {
     "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),
     "vit_copy2d": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _I32, _I64, _I64, _I64, _I64, _F, _P]),
     "vit_dropout_bwd": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _U32, _F, _P]),
+    "vit_mask4_apply": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _I32, _P, _I64, _I64, _F, _P]),
     "vit_relu_bwd": (ctypes.c_int, [_P, _P, _P, _I32, _I64, _P]),
     "vit_gelu_fwd": (ctypes.c_int, [_P, _P, _I64, _P]),
     "vit_gelu_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P]),

@@ -44,11 +44,12 @@ def mask4_empty(m, n, device):
 
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=1.0, beta=0.0, bias=None,
          act=ACT_NONE, aux=None, ldaux=0, res=None, ldres=0, res_rowmod=0, dropout_p=0.0, seed=0, split_k=1,
-         out_group=(0, 0), workspace=None, colsum_part=None, mask_out=None, stream=None):
+         out_group=(0, 0), workspace=None, colsum_part=None, mask_out=None, drop_row_stride=1, stream=None):
     """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  `colsum_part` (f32, colsum_part_rows(m) x n)
     receives per-256-row-block column sums of C as stored — finish with colsum_finish.  `aux` may be a uint8 mask4
     tensor (the ReLU mask saved by the forward); `mask_out` (uint8, mask4_bytes(m, n)) receives C's mask4 (dropout
-    keep bits when dropout_p > 0, else C > 0).  Returns c."""
+    keep bits when dropout_p > 0, else C > 0).  `drop_row_stride` S: output row i draws the dropout bits of row i*S of
+    the full tensor (C = token-0 rows of it).  Returns c."""
     _need_cuda(a, b, c, bias, aux, res, colsum_part, mask_out)
     if a.dtype != b.dtype:
         raise TypeError("gemm: A and B dtypes differ")
@@ -74,6 +75,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=
         if mask_out.dtype != torch.uint8 or mask_out.numel() < mask4_bytes(m, n):
             raise ValueError("gemm: mask_out must be uint8 with >= mask4_bytes(m, n) elements")
         d.mask_out = mask_out.data_ptr()
+    d.dropout_row_stride = drop_row_stride
     if res is not None:
         d.res, d.ldres, d.res_rowmod, d.res_dtype = res.data_ptr(), ldres, res_rowmod, dtype_code(res)
     d.dropout_p, d.dropout_seed = dropout_p, seed & 0xFFFFFFFF
@@ -145,17 +147,20 @@ def layernorm_bwd_parts(rows, cols):
 
 
 def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, drop_p=0.0, drop_seed=0,
-                  partial=None, osum=False, stream=None):
+                  partial=None, osum=False, drop_mask=None, stream=None):
     """dx_out = LN_bwd(dy) (+ dres); drop_out = dx_out * keep (UNSCALED: consumers multiply by 1/(1-p)); returns
     partial [2, parts, cols] f32 (dgamma / dbeta per workgroup) — [3, parts, cols] with `osum`: + the column sums of
     the gradient the next Linear sees (drop_out / (1-p) when given, else dx_out), i.e. its bias gradient.  Reduce
-    with colsum_finish."""
+    with colsum_finish.  `drop_mask` (uint8 mask4): the keep bits saved by the forward, instead of the hash."""
     rows, cols = x.shape
+    if drop_mask is not None and (drop_mask.dtype != torch.uint8 or drop_mask.numel() < mask4_bytes(rows, cols)):
+        raise ValueError("layernorm_bwd: drop_mask must be uint8 with >= mask4_bytes(rows, cols) elements")
     parts = layernorm_bwd_parts(rows, cols)
     if partial is None:
         partial = torch.empty(3 if osum else 2, parts, cols, dtype=torch.float32, device=x.device)
     _lib.call("vit_layernorm_bwd", _ptr(dy), dy.stride(0), _ptr(x), x.stride(0), _ptr(gamma), _ptr(mean), _ptr(rstd),
-              _ptr(dres), _ptr(dx_out), _ptr(drop_out), drop_p, drop_seed & 0xFFFFFFFF, _ptr(partial), int(bool(osum)),
+              _ptr(dres), _ptr(dx_out), _ptr(drop_out), drop_p, drop_seed & 0xFFFFFFFF, _ptr(drop_mask), _ptr(partial),
+              int(bool(osum)),
               rows, cols, dtype_code(x), _stream(stream))
     return partial
 
@@ -220,6 +225,17 @@ def dropout_bwd(x, y, p, seed, scale=None, stream=None):
     scale = 1.0 / (1.0 - p) if scale is None else scale
     _lib.call("vit_dropout_bwd", _ptr(x), _ptr(y), dtype_code(x), x.numel(), p, seed & 0xFFFFFFFF, scale,
               _stream(stream))
+    return y
+
+
+def mask4_apply(x, y, mask, scale=1.0, stream=None):
+    """y = x * mask4 bit * scale for 2-D x, y (any float dtypes, row strides allowed)."""
+    _need_cuda(x, y, mask)
+    rows, cols = x.shape
+    if mask.dtype != torch.uint8 or mask.numel() < mask4_bytes(rows, cols) or tuple(y.shape) != (rows, cols):
+        raise ValueError("mask4_apply: bad mask or output shape")
+    _lib.call("vit_mask4_apply", _ptr(x), x.stride(0), dtype_code(x), _ptr(y), y.stride(0), dtype_code(y), _ptr(mask),
+              rows, cols, scale, _stream(stream))
     return y
 
 

@@ -60,6 +60,11 @@ VIT_DEV uint32_t vit_hash_u32(uint32_t seed, uint32_t idx) {
   x ^= x >> 16;
   return x;
 }
+// VIT_MASK4 bit masks (vit_hip.h): byte ((i/4) * ceil(n/4) + j/4) * 4 + i%4, bit j%4.  A row's 4-column group is one
+// byte and a 4-row x 4-column block one dword (byte = row), so a lane owning 4 columns of a row reads or writes a
+// byte, and over 4 consecutive rows a whole dword.
+VIT_DEV int64_t mask4_byte(int64_t i, int64_t j, int64_t n) { return (((i >> 2) * ((n + 3) >> 2)) + (j >> 2)) * 4 + (i & 3); }
+
 VIT_DEV uint32_t vit_drop_threshold(float p) {
   double t = (double)p * 4294967296.0;
   return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;

@@ -38,12 +38,9 @@ struct EpiParams {
   float* csum;     // v4 fast epilogues: per-tile column sums of C as stored -> csum[tile row][n] (colsum_part)
   int64_t row0;    // global row of local row 0 (split-K tail launch): dropout indices use the global row
   uint8_t* mask_out;  // mask4 of C: dropout keep bits, else (C as stored > 0) — see vit_hip.h
+  int64_t drop_rs;    // dropout index row = (i + row0) * drop_rs (rows of a row-strided view keep their global index)
 };
 
-// mask4 layout of an [m][n] tensor: byte ((i/4) * ceil(n/4) + j/4) * 4 + i%4, bit j%4.  A row's 4-column group is
-// one byte and a 4-row x 4-column block one dword (byte = row), so a lane owning 4 columns of a row reads or writes a
-// byte, and over 4 consecutive rows a whole dword.
-VIT_DEV int64_t mask4_byte(int64_t i, int64_t j, int64_t n) { return (((i >> 2) * ((n + 3) >> 2)) + (j >> 2)) * 4 + (i & 3); }
 
 struct GemmArgs {
   const void* a;
@@ -104,7 +101,7 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
     }
     uint32_t keep = 0xfu;
     if (e.use_drop) {
-      const uint32_t base = (uint32_t)((i + e.row0) * e.n + j);
+      const uint32_t base = (uint32_t)((i + e.row0) * e.drop_rs * e.n + j);
       keep = 0u;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -145,7 +142,7 @@ VIT_DEV void epilogue4(const EpiParams& e, int64_t i, int64_t j, float v[4]) {
       }
       bool k = true;
       if (e.use_drop) {
-        k = vit_hash_u32(e.seed, (uint32_t)((i + e.row0) * e.n + jj)) >= e.drop_thr;
+        k = vit_hash_u32(e.seed, (uint32_t)((i + e.row0) * e.drop_rs * e.n + jj)) >= e.drop_thr;
         x = k ? x * e.drop_scale : 0.f;
       }
       if (e.res) x += ld_any(e.res, e.res_dtype, rrow * e.ldres + jj);
@@ -600,7 +597,7 @@ VIT_DEV uint32_t v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, in
   uint32_t keep = 0u;
   if (KIND == EPI_BDR) {
     if (e.use_drop) {
-      const uint32_t base = (uint32_t)((i + e.row0) * e.n + j);
+      const uint32_t base = (uint32_t)((i + e.row0) * e.drop_rs * e.n + j);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool k = vit_hash_u32(e.seed, base + r) >= e.drop_thr;
@@ -1190,6 +1187,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
   e.csum = nullptr;
   e.row0 = row0;
   e.mask_out = (uint8_t*)d->mask_out;
+  e.drop_rs = d->dropout_row_stride > 1 ? d->dropout_row_stride : 1;
   bool cs_fused = false;
   e.vec = (d->n % 4 == 0) && (d->ldc % 4 == 0) && aligned(d->c, 16) && aligned(d->bias, 16) &&
           (!d->aux || d->aux_dtype == VIT_MASK4 || (d->ldaux % 4 == 0 && aligned(d->aux, 16))) &&

@@ -194,6 +194,23 @@ __global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// y[i][j] = x[i][j] * mask4 bit (i, j) * scale, x any dtype -> y any dtype (4 columns per thread; cols % 4 == 0)
+template <class TI, class TO>
+__global__ __launch_bounds__(256) void mask4_apply_kernel(const TI* __restrict__ x, int64_t ldx, TO* __restrict__ y,
+                                                          int64_t ldy, const uint8_t* __restrict__ mask, int64_t rows,
+                                                          int64_t cols, float scale) {
+  const int64_t nq = cols / 4, total = rows * nq;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / nq, j = (t % nq) * 4;
+    float v[4];
+    ld4<TI>(x + i * ldx + j, v);
+    const uint32_t b = mask[mask4_byte(i, j, cols)];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (b >> r) & 1u ? v[r] * scale : 0.f;
+    st4<TO>(y + i * ldy + j, v);
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void relu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
                                                        T* __restrict__ dx, int64_t n) {
@@ -410,6 +427,22 @@ extern "C" int vit_dropout_bwd(const void* x, void* y, int32_t dtype, int64_t n,
   if (dtype == VIT_BF16) dropout_bwd_kernel<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, n, thr, scale, seed);
   else dropout_bwd_kernel<float><<<grid, 256, 0, s>>>((const float*)x, (float*)y, n, thr, scale, seed);
   return vit::check_launch("vit_dropout_bwd");
+}
+
+extern "C" int vit_mask4_apply(const void* x, int64_t ldx, int32_t x_dtype, void* y, int64_t ldy, int32_t y_dtype,
+                               const void* mask, int64_t rows, int64_t cols, float scale, void* stream) {
+  VIT_REQUIRE(x && y && mask && rows > 0 && cols > 0, "vit_mask4_apply: bad arguments");
+  VIT_REQUIRE(cols % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0, "vit_mask4_apply: cols/ld must be multiples of 4");
+  const unsigned grid = grid_for(rows * (cols / 4), 256, 16384);
+  hipStream_t s = VIT_STREAM(stream);
+  const uint8_t* m = (const uint8_t*)mask;
+#define MA(TI, TO) mask4_apply_kernel<TI, TO><<<grid, 256, 0, s>>>((const TI*)x, ldx, (TO*)y, ldy, m, rows, cols, scale)
+  if (x_dtype == VIT_BF16 && y_dtype == VIT_BF16) MA(bf16_t, bf16_t);
+  else if (x_dtype == VIT_BF16) MA(bf16_t, float);
+  else if (y_dtype == VIT_BF16) MA(float, bf16_t);
+  else MA(float, float);
+#undef MA
+  return vit::check_launch("vit_mask4_apply");
 }
 
 extern "C" int vit_relu_bwd(const void* dy, const void* y, void* dx, int32_t dtype, int64_t n, void* stream) {

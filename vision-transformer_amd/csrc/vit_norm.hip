@@ -72,13 +72,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const T* __restrict__ dres, T* __restrict__ dx_out,
                                                      T* __restrict__ drop_out, uint32_t drop_thr, float drop_scale,
-                                                     uint32_t drop_seed, float* __restrict__ partial, int osum,
+                                                     uint32_t drop_seed, const uint8_t* __restrict__ drop_mask,
+                                                     float* __restrict__ partial, int osum,
                                                      int64_t parts, int64_t rows, int64_t cols) {
   __shared__ float red[3][256 * NV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t rows_per_part = (rows + parts - 1) / parts;
+  // whole groups of 4 rows per block and per wave step: a wave's 4 consecutive rows share one dword of a mask4
+  const int64_t rows_per_part = (((rows + parts - 1) / parts) + 3) & ~(int64_t)3;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_part, r1 = min(rows, r0 + rows_per_part);
   float dg[NV][4], db[NV][4], os[NV][4], gm[NV][4];
+  uint32_t mw[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) mw[k] = 0u;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int64_t c = ((int64_t)k * 64 + lane) * 4;
@@ -87,7 +92,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
     if (c < cols) ld4<float>(gamma + c, gm[k]);
     else gm[k][0] = gm[k][1] = gm[k][2] = gm[k][3] = 0.f;
   }
-  for (int64_t row = r0 + w; row < r1; row += 4) {
+  for (int64_t it = 0; r0 + 4 * (w + 4 * (it >> 2)) < r1; ++it) {
+    const int64_t g4 = r0 + 4 * (w + 4 * (it >> 2)), row = g4 + (it & 3);
+    if (row >= r1) continue;
+    if (drop_mask && (it & 3) == 0) {                  // the dword of rows g4..g4+3 for each of the lane's columns
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t c = ((int64_t)k * 64 + lane) * 4;
+        mw[k] = c < cols ? *reinterpret_cast<const uint32_t*>(drop_mask + mask4_byte(g4, c, cols)) : 0u;
+      }
+    }
     const float mu = mean[row], rs = rstd[row];
     // every load of the row (x, dy, residual gradient) is issued before the first reduction: one memory round trip
     // per row instead of two
@@ -132,10 +146,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
           // the dropout mask on the value as stored, WITHOUT the 1/(1-p) scale: exact in any dtype (the scale is
           // applied by the consumers — GEMM alpha, and the column sums below), so the masked gradient adds no
           // rounding of its own
-          const uint32_t base = (uint32_t)(row * cols + c);
           float dd[4];
+          if (drop_mask) {                    // the forward's keep bits (mask4 of the producing GEMM's dropout)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? as_stored<T>(o[r]) : 0.f;
+            for (int r = 0; r < 4; ++r) dd[r] = (mw[k] >> (8 * (it & 3) + r)) & 1u ? as_stored<T>(o[r]) : 0.f;
+          } else {
+            const uint32_t base = (uint32_t)(row * cols + c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dd[r] = vit_hash_u32(drop_seed, base + r) >= drop_thr ? as_stored<T>(o[r]) : 0.f;
+          }
           st4<T>(drop_out + row * cols + c, dd);
           if (osum) {
 #pragma unroll
@@ -227,7 +246,8 @@ extern "C" int vit_layernorm_fwd(const void* x, int64_t ldx, const float* gamma,
 
 extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* gamma,
                                  const float* mean, const float* rstd, const void* dres, void* dx_out,
-                                 void* drop_out, float drop_p, uint32_t drop_seed, float* partial, int32_t osum,
+                                 void* drop_out, float drop_p, uint32_t drop_seed, const void* drop_mask,
+                                 float* partial, int32_t osum,
                                  int64_t rows, int64_t cols, int32_t dtype, void* stream) {
   VIT_REQUIRE(dy && x && gamma && mean && rstd && dx_out && partial && rows > 0 && cols > 0,
               "vit_layernorm_bwd: bad arguments");
@@ -243,14 +263,14 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
 #define CALLB(NV)                                                                                               \
   ln_bwd_kernel<bf16_t, NV><<<(unsigned)parts, 256, 0, s>>>(                                                    \
       (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
-      (bf16_t*)drop_out, thr, scale, drop_seed, partial, osum != 0, parts, rows, cols)
+      (bf16_t*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLB)
 #undef CALLB
   } else {
 #define CALLF(NV)                                                                                            \
   ln_bwd_kernel<float, NV><<<(unsigned)parts, 256, 0, s>>>(                                                  \
       (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out,   \
-      (float*)drop_out, thr, scale, drop_seed, partial, osum != 0, parts, rows, cols)
+      (float*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLF)
 #undef CALLF
   }
