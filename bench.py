@@ -15,7 +15,7 @@ a GPU.  Rank 0 prints ONE JSON line.
 Live roofline: HIP events on the compute stream bracket every hot launch of the step, grouped into families
 (forward / dgrad / wgrad GEMMs, attention fwd/bwd, LayerNorm fwd/bwd), each launch carrying its algorithmic FLOPs and
 HBM bytes.  `roofline` reports the family that takes the most time; `roofline_families`
-reports all of them.  `traffic` is the measured HBM bytes of that family (rocprofv3 PMC passes committed under
+reports all of them.  `traffic` is the measured HBM bytes per launch of that family (rocprofv3 PMC passes under
 profiles/ for this exact workload), or null when no such profile exists.
 `cpu_baseline` times the repo's own host training step (train.py `time_steps`, VisionTransformer/_cpu.py) on all the
 cores this process may use: BASELINE config 1 exactly (ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 steps) and a bounded
@@ -310,9 +310,14 @@ def run(args, rank, world, local):
                     ach, pk, unit, bound = d["hbm_gbs_algorithmic"], PEAK_HBM / 1e9, "GB/s", "hbm"
                 out["roofline"] = {
                     "bound": bound, "family": dom, "achieved": ach, "peak": pk, "unit": unit,
-                    "frac": round(ach / pk, 4), "traffic": traffic,
-                    "traffic_unit": "HBM bytes per step for this family (rocprofv3 PMC)",
+                    "frac": round(ach / pk, 4),
+                    # per launch, like `achieved`: the PMC family's HBM bytes per step / this family's launches
+                    "traffic": int(traffic / d["launches_per_step"]) if traffic is not None else None,
+                    "traffic_unit": "HBM bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                    "traffic_per_step": traffic,
+                    "algorithmic_bytes_per_launch": int(d["bytes_per_step"] / d["launches_per_step"]),
                     "algorithmic_bytes_per_step": int(d["bytes_per_step"]),
+                    "pmc_mfma_busy_frac": pmc.get("mfma_busy_frac") if pmc else None,
                     "traffic_source": f"profiles/pmc_{key}.json" if traffic is not None else None,
                     "ms_per_step": d["ms_per_step"], "launches_per_step": d["launches_per_step"],
                     "avg_launch_us": d["avg_launch_us"],

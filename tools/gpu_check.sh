@@ -22,6 +22,9 @@ for s in $STEPS; do
     model) timeout -k 10 900 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_dropin.py -x -v -m gpu \
              -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/model.log" 2>&1 ;;
     ln) timeout -k 10 300 python -u tools/ln_bench.py > "$OUT/ln.log" 2>&1 ;;
+    lnab) for v in ${LN_VARIANTS:-}; do
+            VIT_HIP_LIB=tools/variants/libvit_hip_$v.so timeout -k 10 120 python -u tools/ln_bench.py > "$OUT/ln_$v.log" 2>&1 || break
+          done ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     bench) timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \

@@ -43,6 +43,27 @@ def family(name):
     return "other"
 
 
+def short(name):
+    n = re.sub(r"\(anonymous namespace\)::", "", name)
+    n = re.sub(r"^void ", "", n)
+    return re.sub(r"\((?!anonymous).*$", "", n)[:90]
+
+
+def derived(cs):
+    d = {}
+    if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+        rd, wr = 2 * cs["FETCH_SIZE"] * 1024, cs["WRITE_SIZE"] * 1024
+        d.update(hbm_read_bytes_per_step=int(rd), hbm_write_bytes_per_step=int(wr), hbm_bytes_per_step=int(rd + wr))
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs:
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs: active GPU cycles = GRBM / 8; 1024 SIMDs
+        d["mfma_busy_frac"] = round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] * 8 / (1024 * cs["GRBM_GUI_ACTIVE"]), 4)
+    if "SQ_WAIT_ANY" in cs and "SQ_WAVE_CYCLES" in cs:
+        d["wave_frac_parked_waitcnt_barrier"] = round(cs["SQ_WAIT_ANY"] / cs["SQ_WAVE_CYCLES"], 4)
+    if "SQ_WAIT_INST_ANY" in cs and "SQ_WAVE_CYCLES" in cs:
+        d["wave_frac_issue_stalled"] = round(cs["SQ_WAIT_INST_ANY"] / cs["SQ_WAVE_CYCLES"], 4)
+    return d
+
+
 def load(dirs):
     """{counter: {kernel: value summed over its dispatches}}"""
     vals = {}
@@ -58,31 +79,24 @@ def load(dirs):
 def main():
     key, steps, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
     vals = load(sys.argv[4:])
-    fams = {}
+    fams, kers = {}, {}
     for c, per in vals.items():
         for k, v in per.items():
             f = fams.setdefault(family(k), {})
             f[c] = f.get(c, 0.0) + v / steps
-    res = {}
-    for f, cs in fams.items():
-        d = {"counters_per_step": {c: round(v, 1) for c, v in sorted(cs.items())}}
-        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-            rd, wr = 2 * cs["FETCH_SIZE"] * 1024, cs["WRITE_SIZE"] * 1024
-            d.update(hbm_read_bytes_per_step=int(rd), hbm_write_bytes_per_step=int(wr),
-                     hbm_bytes_per_step=int(rd + wr))
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs:
-            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: active GPU cycles = GRBM / 8; 1024 SIMDs
-            d["mfma_busy_frac"] = round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] * 8 / (1024 * cs["GRBM_GUI_ACTIVE"]), 4)
-        if "SQ_WAIT_ANY" in cs and "SQ_WAVE_CYCLES" in cs:
-            d["wave_frac_parked_waitcnt_barrier"] = round(cs["SQ_WAIT_ANY"] / cs["SQ_WAVE_CYCLES"], 4)
-        if "SQ_WAIT_INST_ANY" in cs and "SQ_WAVE_CYCLES" in cs:
-            d["wave_frac_issue_stalled"] = round(cs["SQ_WAIT_INST_ANY"] / cs["SQ_WAVE_CYCLES"], 4)
-        res[f] = d
+            kk = kers.setdefault(short(k), {})
+            kk[c] = kk.get(c, 0.0) + v / steps
+    res = {f: dict(counters_per_step={c: round(v, 1) for c, v in sorted(cs.items())}, **derived(cs))
+           for f, cs in fams.items()}
+    kres = {k: dict(family=family(k), **derived(cs)) for k, cs in kers.items()}
+    kres = dict(sorted(kres.items(), key=lambda kv: -kv[1].get("hbm_bytes_per_step", 0)))
     json.dump({"workload_key": key, "steps_divisor": steps,
                "method": "rocprofv3 --pmc, one counter group per pass over bench.py; per-kernel sums / steps; "
                          "FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; KiB -> bytes",
-               "families": res}, open(out, "w"), indent=1)
+               "families": res, "kernels": kres}, open(out, "w"), indent=1)
     print(json.dumps({f: {k: v for k, v in d.items() if k != "counters_per_step"} for f, d in res.items()}, indent=1))
+    for k, d in list(kres.items())[:16]:
+        print(f"{d.get('hbm_bytes_per_step', 0) / 1e6:9.1f} MB/step  mfma {d.get('mfma_busy_frac', 0):.3f}  {k}")
 
 
 if __name__ == "__main__":

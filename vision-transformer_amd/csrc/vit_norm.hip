@@ -63,6 +63,31 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, in
   }
 }
 
+// 4 consecutive values of T held as loaded (bf16: 2 dwords), unpacked to fp32 when used
+template <class T> struct Raw4;
+template <> struct Raw4<bf16_t> {
+  using type = uint2;
+  static VIT_DEV uint2 zero() { return make_uint2(0u, 0u); }
+  static VIT_DEV uint2 load(const bf16_t* p) { return *reinterpret_cast<const uint2*>(p); }
+  static VIT_DEV void unpack(uint2 u, float (&v)[4]) {
+    v[0] = __uint_as_float(u.x << 16);
+    v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16);
+    v[3] = __uint_as_float(u.y & 0xffff0000u);
+  }
+};
+template <> struct Raw4<float> {
+  using type = f32x4;
+  static VIT_DEV f32x4 zero() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+  static VIT_DEV f32x4 load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+  static VIT_DEV void unpack(f32x4 u, float (&v)[4]) {
+    v[0] = u[0];
+    v[1] = u[1];
+    v[2] = u[2];
+    v[3] = u[3];
+  }
+};
+
 // the value of v as stored in T (bf16 rounds to nearest even)
 template <class T> VIT_DEV float as_stored(float v) { return sizeof(T) == 2 ? bf2f(f2bf(v)) : v; }
 
@@ -92,30 +117,48 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
     if (c < cols) ld4<float>(gamma + c, gm[k]);
     else gm[k][0] = gm[k][1] = gm[k][2] = gm[k][3] = 0.f;
   }
-  for (int64_t it = 0; r0 + 4 * (w + 4 * (it >> 2)) < r1; ++it) {
-    const int64_t g4 = r0 + 4 * (w + 4 * (it >> 2)), row = g4 + (it & 3);
-    if (row >= r1) continue;
-    if (drop_mask && (it & 3) == 0) {                  // the dword of rows g4..g4+3 for each of the lane's columns
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int64_t c = ((int64_t)k * 64 + lane) * 4;
-        mw[k] = c < cols ? *reinterpret_cast<const uint32_t*>(drop_mask + mask4_byte(g4, c, cols)) : 0u;
-      }
-    }
-    const float mu = mean[row], rs = rstd[row];
-    // every load of the row (x, dy, residual gradient) is issued before the first reduction: one memory round trip
-    // per row instead of two
-    float xv[NV][4], dv[NV][4], rv[NV][4];
+  // Wave w walks rows r0 + 4w + 16q + (0..3), q = 0, 1, ...: the next row's x / dy / residual (raw, packed) and mask
+  // dword are loaded while the current row is reduced and stored — one memory latency per wave, not one per row.
+  auto row_of = [&](int64_t n) { return r0 + 4 * (w + 4 * (n >> 2)) + (n & 3); };
+  using R4 = typename Raw4<T>::type;
+  R4 xc[NV], dc[NV], rc[NV], xn[NV], dn[NV], rn[NV];
+  uint32_t mn[NV];
+  float mu_n = 0.f, rs_n = 0.f;
+  auto load_row = [&](int64_t row, R4 (&xa)[NV], R4 (&da)[NV], R4 (&ra)[NV], uint32_t (&ma)[NV], float& mu_,
+                      float& rs_) {
+    mu_ = mean[row];
+    rs_ = rstd[row];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int64_t c = ((int64_t)k * 64 + lane) * 4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xv[k][r] = dv[k][r] = rv[k][r] = 0.f;
+      xa[k] = da[k] = ra[k] = Raw4<T>::zero();
       if (c < cols) {
-        ld4<T>(x + row * ldx + c, xv[k]);
-        ld4<T>(dy + row * lddy + c, dv[k]);
-        if (dres) ld4<T>(dres + row * cols + c, rv[k]);
+        xa[k] = Raw4<T>::load(x + row * ldx + c);
+        da[k] = Raw4<T>::load(dy + row * lddy + c);
+        if (dres) ra[k] = Raw4<T>::load(dres + row * cols + c);
+        if (drop_mask && (row & 3) == 0)
+          ma[k] = *reinterpret_cast<const uint32_t*>(drop_mask + mask4_byte(row, c, cols));
       }
+    }
+  };
+  if (row_of(0) < r1) load_row(row_of(0), xn, dn, rn, mn, mu_n, rs_n);
+  for (int64_t n = 0; row_of(n) < r1; ++n) {
+    const int64_t row = row_of(n);
+    const float mu = mu_n, rs = rs_n;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      xc[k] = xn[k];
+      dc[k] = dn[k];
+      rc[k] = rn[k];
+      if ((row & 3) == 0) mw[k] = mn[k];
+    }
+    if (row_of(n + 1) < r1) load_row(row_of(n + 1), xn, dn, rn, mn, mu_n, rs_n);
+    float xv[NV][4], dv[NV][4], rv[NV][4];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      Raw4<T>::unpack(xc[k], xv[k]);
+      Raw4<T>::unpack(dc[k], dv[k]);
+      Raw4<T>::unpack(rc[k], rv[k]);
     }
     float sa = 0.f, sb = 0.f;
 #pragma unroll
@@ -149,7 +192,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
           float dd[4];
           if (drop_mask) {                    // the forward's keep bits (mask4 of the producing GEMM's dropout)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dd[r] = (mw[k] >> (8 * (it & 3) + r)) & 1u ? as_stored<T>(o[r]) : 0.f;
+            for (int r = 0; r < 4; ++r) dd[r] = (mw[k] >> (8 * (row & 3) + r)) & 1u ? as_stored<T>(o[r]) : 0.f;
           } else {
             const uint32_t base = (uint32_t)(row * cols + c);
 #pragma unroll
