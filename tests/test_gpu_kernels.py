@@ -341,6 +341,47 @@ def test_gemm_mask4_produce_consume(monkeypatch, variant):
     assert torch.equal(p_m, p_ref)
 
 
+@pytest.mark.parametrize("variant", ["plain", "plain_cs", "bias_relu_mask", "aux_cs", "auxm_cs", "bias_drop_res_mask",
+                                     "grouped"])
+def test_gemm_persistent_matches_one_per_item(monkeypatch, variant):
+    """The wide-epilogue kinds run on a persistent grid (one workgroup per CU looping over its tiles, the next tile's
+    first stages staged during the current tile's epilogue).  With more tiles than CUs (ragged last tile row), outputs,
+    masks and fused column sums equal the one-workgroup-per-tile launch (VIT_GEMM_PERSIST=0) bit for bit; integer
+    data makes the plain product exact."""
+    g = torch.Generator().manual_seed(17)
+    M, N, K = (4200, 4096, 192) if variant == "grouped" else (23 * 256 + 100, 3072, 256)   # 272 / 288 tiles
+    a = _ints((M, K), gen=g)
+    b = _ints((N, K), gen=g)
+    bias = _ints((N,), gen=g, dtype=torch.float32)
+    aux = _ints((M, N), gen=g)
+    res = _ints((M, N), gen=g)
+    mask_in = torch.randint(0, 256, (_ops.mask4_bytes(M, N),), generator=g, dtype=torch.uint8).to(DEV)
+    results = []
+    for persist in ("1", "0"):
+        monkeypatch.setenv("VIT_GEMM_PERSIST", persist)
+        c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        part = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
+        mask = torch.full((_ops.mask4_bytes(M, N),), 0xAA, dtype=torch.uint8, device=DEV)
+        if variant in ("aux_cs", "auxm_cs"):             # dgrad layout (B row-strided), ReLU-backward mask
+            bt = b.t().contiguous()
+            kw = dict(aux=aux, ldaux=N) if variant == "aux_cs" else dict(aux=mask_in)
+            _ops.gemm(a, bt, c, M, N, K, K, N, N, b_kcontig=False, colsum_part=part, alpha=0.5, **kw)
+        else:
+            kw = {"plain_cs": dict(colsum_part=part), "bias_relu_mask": dict(bias=bias, act=_ops.ACT_RELU, mask_out=mask),
+                  "bias_drop_res_mask": dict(bias=bias, dropout_p=0.2, seed=5, res=res, ldres=N, mask_out=mask)}.get(
+                      variant, {})
+            _ops.gemm(a, b, c, M, N, K, K, K, N, **kw)
+        results.append((c, part if "cs" in variant else None, mask if "mask" in variant else None))
+    (c1, p1, m1), (c0, p0, m0) = results
+    assert torch.equal(c1, c0)
+    if p1 is not None:
+        assert torch.equal(p1, p0)
+    if m1 is not None:
+        assert torch.equal(m1, m0)
+    if variant in ("plain", "grouped"):
+        assert torch.equal(c1, (a.double() @ b.double().t()).float().bfloat16())
+
+
 def _attn_ref(qkv, B, T, H, hd, scale):
     D = H * hd
     q, k, v = qkv.float().view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)

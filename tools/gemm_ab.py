@@ -25,6 +25,9 @@ SHAPES = {  # name: m, n, k, a_kcontig, b_kcontig, epilogue
     "wgrad_fc1": (4 * D, D, M, False, False, "wgrad"), "wgrad_fc2": (D, 4 * D, M, False, False, "wgrad"),
     "wgrad_qkv": (3 * D, D, M, False, False, "wgrad"), "wgrad_proj": (D, D, M, False, False, "wgrad"),
     "sq8192": (8192, 8192, 8192, True, True, None),
+    # one-round grids (epilogue cost vs how many CUs store at once)
+    "fc1m_t24": (512, 4 * D, D, True, True, "bias_relu_m"), "fc1m_t96": (2048, 4 * D, D, True, True, "bias_relu_m"),
+    "fc1m_t252": (5376, 4 * D, D, True, True, "bias_relu_m"), "fc1m_t504": (10752, 4 * D, D, True, True, "bias_relu_m"),
 }
 
 
@@ -74,9 +77,9 @@ def main():
     specs = [(s.split("@")[0], dict(kv.split("=") for kv in s.split("@")[1].split(",")) if "@" in s else {})
              for s in args.libs]
     cache = {}
-    libs = [cache.setdefault(p, load(p)) for p, _ in specs]
+    libs = [None if p == "torch" else cache.setdefault(p, load(p)) for p, _ in specs]
     envs = [e for _, e in specs]
-    names = [os.path.basename(p).replace("libvit_hip_", "").replace(".so", "") +
+    names = ["torch" if p == "torch" else os.path.basename(p).replace("libvit_hip_", "").replace(".so", "") +
              ("@" + ",".join(f"{k}={v}" for k, v in e.items()) if e else "") for p, e in specs]
     ws = torch.empty(96 << 20, dtype=torch.float32, device="cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -91,18 +94,26 @@ def main():
         mask = torch.randint(0, 256, (4 * ((m + 3) // 4) * ((n + 3) // 4),), device="cuda", generator=g,
                              dtype=torch.uint8)
         c = torch.empty(m, n, dtype=torch.float32 if epi == "wgrad" else torch.bfloat16, device="cuda")
-        split = libs[0].vit_gemm_split_k_hint(m, n, k, _lib.BF16) if epi == "wgrad" else 1
+        split = next(l for l in libs if l is not None).vit_gemm_split_k_hint(m, n, k, _lib.BF16) if epi == "wgrad" else 1
         times = {nm: [] for nm in names}
         outs = {}
         for rep in range(args.reps + 2):
             for nm, lib, env in zip(names, libs, envs):
                 saved = {kk: os.environ.get(kk) for kk in env}
                 os.environ.update(env)
-                d = desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res, mask)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                rc = lib.vit_gemm(ctypes.byref(d), stream)
-                e1.record()
+                if lib is None:   # "torch": hipBLASLt plain GEMM of the same operands (no epilogue), reference only
+                    at = a if akc else a.t()
+                    bt = b.t() if bkc else b
+                    e0.record()
+                    torch.mm(at, bt, out=c if c.dtype == torch.bfloat16 else None)
+                    e1.record()
+                    rc = 0
+                else:
+                    d = desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res, mask)
+                    e0.record()
+                    rc = lib.vit_gemm(ctypes.byref(d), stream)
+                    e1.record()
                 torch.cuda.synchronize()
                 for kk, vv in saved.items():
                     if vv is None:
@@ -120,6 +131,8 @@ def main():
         for nm in names:
             t = sorted(times[nm])[len(times[nm]) // 2]
             same = "=" if torch.equal(outs[nm], outs[names[0]]) else "!"
+            if nm == "torch":
+                same = "~"
             line += f" | {nm}: {t * 1e6:7.1f}us {flop / t / 1e12:7.1f}TF {same}"
         print(line, flush=True)
 

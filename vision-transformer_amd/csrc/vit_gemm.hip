@@ -35,6 +35,7 @@ struct EpiParams {
   int use_drop;
   int64_t grp, grp_stride;
   int vec;  // all row strides/pointers allow 4-wide vector access
+  int vec8; // ... and 8-wide (16 B of bf16): the v4 wide row epilogue (required for the fast bf16 kinds)
   float* csum;     // v4 fast epilogues: per-tile column sums of C as stored -> csum[tile row][n] (colsum_part)
   int64_t row0;    // global row of local row 0 (split-K tail launch): dropout indices use the global row
   uint8_t* mask_out;  // mask4 of C: dropout keep bits, else (C as stored > 0) — see vit_hip.h
@@ -51,6 +52,7 @@ struct GemmArgs {
                              // column-major inside a group (group_m = 1: row-major)
   int64_t kt_per_split;  // k-tiles per split
   float* ws;             // split-K slabs [split][M][N]
+  int64_t nitems;        // v4: tiles x K-slices (work items; a persistent grid loops over them)
 };
 
 VIT_DEV float ld_any(const void* p, int dt, int64_t idx) {
@@ -557,9 +559,11 @@ VIT_DEV void unpack_bf16x4(uint2 u, float (&a)[4]) {
 
 // Returns the row's mask4 nibble (dropout keep bits for EPI_BDR with dropout, else stored value > 0) for the fast
 // kinds that produce one (the caller stores 4 rows' nibbles as one dword); 0 otherwise.
-template <class TO, int KIND>
+// ACT (EPI_BIAS_ACT only): 0 none, 1 ReLU, 2 GELU(erf) — a template argument, so the row code carries no runtime
+// activation branches (the erf body was inlined four times behind them in every unrolled row).
+template <class TO, int KIND, int ACT>
 VIT_DEV uint32_t v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, int64_t j, const float (&b4)[4],
-                            bool relu, bool gelu, float v[4], uint2 pre = make_uint2(0u, 0u)) {
+                            float v[4], uint2 pre = make_uint2(0u, 0u)) {
   if (KIND == EPI_GENERAL) {
     epilogue4<TO>(e, i, j, v);
     return 0u;
@@ -575,14 +579,12 @@ VIT_DEV uint32_t v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, in
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] += b4[r];
   }
-  if (KIND == EPI_BIAS_ACT) {
-    if (relu) {
+  if (KIND == EPI_BIAS_ACT && ACT == 1) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-    } else if (gelu) {
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+  } else if (KIND == EPI_BIAS_ACT && ACT == 2) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
-    }
+    for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
   }
   if (KIND == EPI_AUX) {                            // aux is bf16 (host-checked), prefetched
     float a[4];
@@ -736,26 +738,497 @@ VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <bool AKC, bool BKC, class TO, int KIND>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem4[V4_SLOTS * HALF];
-  const int tid = threadIdx.x, lane = tid & 63;
+// Diagnostic build only (-DVIT_GEMM_STAMPS): wave 0 of every v4 workgroup records s_memtime at fixed points into a
+// buffer of its own (nothing in the kernel reads it back; no output depends on it) — MI355X_MICROARCH.md 'DVFS
+// give-back' (6).  Read with vit_gemm_debug_stamps().
+// The kernel accumulates, per workgroup and in registers, the cycles spent in each interval (V4_ACC(K): slot K += now -
+// previous stamp) and stores the 8 sums at its end: 0 k-loop, 1 next-tile stage issue, 2 epilogue, 3 restage + wait,
+// 4 loop-top barrier, 5 first prologue, 6 items processed, 7 tail (last epilogue to all stores retired).
+#ifdef VIT_GEMM_STAMPS
+__device__ unsigned long long vit_stamps[16384 * 8];
+#define V4_STAMP(K) do {} while (0)
+#define V4_ACC(K)                                                                              \
+  do {                                                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                              \
+    st_acc_[K] += now_ - st_last_;                                                             \
+    st_last_ = now_;                                                                           \
+  } while (0)
+#else
+#define V4_STAMP(K) do {} while (0)
+#define V4_ACC(K) do {} while (0)
+#endif
+
+// Row-contiguous epilogue through LDS, one 128-row half of the tile per pass: the fragment layout (16 rows x 32 B
+// per store instruction) becomes 1 row x 256 columns per wave instruction, so output stores and residual / mask
+// loads are full-line.  Image: [128][256] fp32, 16-B chunk index XOR (row & 15) -> conflict-free b128 writes
+// (8 rows per lane group) and reads (16 chunks of one row per group).  A pass's 16 row reads are issued together
+// before any row is processed: one row at a time (read, lgkmcnt(0), math, store) was a serial LDS-latency chain of
+// ~8 us per tile at two waves per SIMD.
+template <class TO, int KIND, int ACT>
+VIT_DEV void v4_epilogue(const EpiParams& e, const GemmArgs& g, const f32x4 (&acc)[2][2][4][2], bf16_t* smem4,
+                         int tid, int64_t i0, int64_t j0, int64_t tm) {
+  const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  // One-dimensional grid of tiles x K-slices.  Workgroups are dealt round-robin over the 8 XCDs (linear id % 8); the
-  // bijective remap gives each XCD a contiguous range of `bid`, and bid is split-major (all tiles of K-slice 0, then
-  // slice 1, ...), so the ~32 workgroups an XCD runs at once are tiles of ONE K-slice that share A row panels and B
-  // column panels, walking k in step: the XCD's L2 serves the re-reads.  (With the slices on gridDim.y the hardware's
-  // linear order x + y * gridDim.x scattered a panel's tiles over XCDs: the weight-gradient GEMMs fetched ~3.5x their
-  // operand bytes from beyond L2.)
-  const int64_t nwg = gridDim.x, orig = blockIdx.x;
-  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int64_t bid_all = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  float* ep = reinterpret_cast<float*>(smem4);
+  const int64_t jcol = j0 + 4 * lane;
+  float b4[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias && jcol < e.n) ld4<float>(e.bias + jcol, b4);
+  // second-operand rows of both passes, in flight before the LDS round trip (see v4_has_pre)
+  uint2 pre[2][16];
+  const bool has_pre = v4_has_pre<KIND>(e);
+  // fused column sums of C as stored (the bias gradient of the Linear whose input gradient C is)
+  const bool cs_on = (KIND == EPI_PLAIN || KIND == EPI_BIAS_ACT || KIND == EPI_AUX || KIND == EPI_AUXM ||
+                      KIND == EPI_BDR) && e.csum != nullptr;
+  // mask4 of C: 4 rows' nibbles of this lane's column group -> one dword store per 4 rows (EPI_GENERAL writes it in
+  // epilogue4, the split-K reduce after EPI_SLAB)
+  const bool mk_on = KIND != EPI_GENERAL && KIND != EPI_SLAB && e.mask_out != nullptr;
+  uint32_t mword = 0u;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (has_pre) {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        if (KIND != EPI_AUXM) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
+        else if ((rr & 3) == 0) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
+        else pre[mh][rr] = make_uint2(pre[mh][rr & ~3].x >> (8 * (rr & 3)), 0u);
+      }
+  }
+  __syncthreads();                                        // every wave's k-loop LDS reads are done, no DMA pending
+  V4_STAMP(3);
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const int row = wr * 64 + x * 16 + (lane & 15);
+          const int chunk = (nh * 128 + wc * 32 + y * 16) / 4 + (lane >> 4);
+          *reinterpret_cast<f32x4*>(ep + row * 256 + ((chunk ^ (row & 15)) << 2)) = acc[mh][nh][x][y];
+        }
+    __syncthreads();
+    f32x4 rv[16];
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const int row = wave * 16 + rr;
+      rv[rr] = *reinterpret_cast<const f32x4*>(ep + row * 256 + ((lane ^ (row & 15)) << 2));
+    }
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const int row = wave * 16 + rr;
+      float v[4] = {rv[rr][0], rv[rr][1], rv[rr][2], rv[rr][3]};
+      const int64_t i = i0 + mh * 128 + row, j = j0 + 4 * lane;
+#ifdef VIT_GEMM_NOEPI
+      if (v[0] != 1234.5f) continue;
+#endif
+      const uint32_t nib = v4_epi_row<TO, KIND, ACT>(e, g, i, j, b4, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
+      if (mk_on) {
+        mword |= (nib & 0xfu) << (8 * (rr & 3));
+        if ((rr & 3) == 3) {                            // rows i-3..i: one dword (row groups are allocated whole)
+          if (i - 3 < e.m && j < e.n)
+            *reinterpret_cast<uint32_t*>(e.mask_out + mask4_byte(i - 3, j, e.n)) = mword;
+          mword = 0u;
+        }
+      }
+      if (cs_on && i < e.m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[r] += sizeof(TO) == 2 ? bf2f(f2bf(v[r])) : v[r];
+      }
+    }
+    if (mh == 0) __syncthreads();
+  }
+  V4_STAMP(4);
+  if (cs_on) {
+    // per-lane sums of the wave's 32 rows -> LDS -> the 8 wave sums added in wave order: one row of csum per tile
+    __syncthreads();
+    *reinterpret_cast<f32x4*>(ep + wave * 256 + 4 * lane) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    __syncthreads();
+    if (tid < 256 && j0 + tid < e.n) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) sum += ep[w8 * 256 + tid];
+      e.csum[tm * e.n + j0 + tid] = sum;
+    }
+  }
+}
+
+// LDS-only workgroup barrier for the epilogue: retires this wave's LDS operations, not its global loads, so the
+// second-operand prefetch stays in flight across it (__syncthreads()' fence waits vmcnt(0)).  The "memory" clobber
+// keeps the compiler from moving LDS accesses across it.
+#define V4_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+// Wide row epilogue (bf16 output, fast kinds, rows 8-element aligned — e.vec8): one wave instruction stores two
+// whole 256-column rows, 16 B per lane (lanes 0-31 row r, lanes 32-63 row r + 1).  Per-CU store throughput is set by
+// the number of store instructions (tools/gemm_stamps.py: 8-B-per-lane rows took ~16k cycles per 256^2 tile, half
+// the K = 768 k-loop), so 16-B stores halve it (cdna_hip_programming.md T21).
+template <int KIND>
+VIT_DEV uint4 v4_pre_load8(const EpiParams& e, int64_t i, int64_t j) {
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (i >= e.m || j >= e.n) return r;
+  if (KIND == EPI_AUXM) {        // the dwords of column groups j/4 and j/4 + 1 of row group i/4 (8-B aligned: vec8)
+    const uint2 x = *reinterpret_cast<const uint2*>((const uint8_t*)e.aux + mask4_byte(i & ~(int64_t)3, j, e.n));
+    r.x = x.x;
+    r.y = x.y;
+    return r;
+  }
+  const bf16_t* p = KIND == EPI_AUX ? (const bf16_t*)e.aux + i * e.ldaux + j : (const bf16_t*)e.res + i * e.ldres + j;
+  return *reinterpret_cast<const uint4*>(p);
+}
+
+VIT_DEV void unpack_bf16x8(uint4 u, float (&a)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[2 * q] = __uint_as_float(w[q] << 16);
+    a[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32, RNE — the same rounding as f2bf)
+VIT_DEV uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2_t));
+}
+
+// One row piece of 8 columns (v: fp32 accumulators in, the values as stored out when MK or CS need them).  Returns
+// the 8 mask bits (bit r = column j + r) when MK: dropout keep bits for EPI_BDR with dropout, else stored value > 0.
+// sh = 8 * (i % 4), the row's byte in a mask4 dword (EPI_AUXM).  The caller checks the row / column bounds.
+template <int KIND, int ACT, bool MK, bool CS>
+VIT_DEV uint32_t v4_epi_row8(const EpiParams& e, int64_t i, int64_t j, bf16_t* cp, const float (&b8)[8],
+                             float (&v)[8], uint4 pre, int sh) {
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] *= e.alpha;
+  if (KIND == EPI_BIAS_ACT || KIND == EPI_BDR) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += b8[r];
+  }
+  if (KIND == EPI_BIAS_ACT && ACT == 1) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+  } else if (KIND == EPI_BIAS_ACT && ACT == 2) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
+  }
+  if (KIND == EPI_AUX) {
+    float a[8];
+    unpack_bf16x8(pre, a);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = a[r] > 0.f ? v[r] : 0.f;
+  }
+  if (KIND == EPI_AUXM) {
+    const uint32_t bits = ((pre.x >> sh) & 0xfu) | (((pre.y >> sh) & 0xfu) << 4);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = (bits >> r) & 1u ? v[r] : 0.f;
+  }
+  uint32_t keep = 0u;
+  if (KIND == EPI_BDR) {
+    if (e.use_drop) {
+      const uint32_t base = (uint32_t)((i + e.row0) * e.drop_rs * e.n + j);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const bool k = vit_hash_u32(e.seed, base + r) >= e.drop_thr;
+        keep |= (uint32_t)k << r;
+        v[r] = k ? v[r] * e.drop_scale : 0.f;
+      }
+    }
+    if (e.res) {
+      float a[8];
+      unpack_bf16x8(pre, a);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] += a[r];
+    }
+  }
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
+#ifdef VIT_EPI_NOSTORE   // ablation build: everything but the output store (values kept live)
+  asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+#else
+  *reinterpret_cast<uint4*>(cp) = make_uint4(w[0], w[1], w[2], w[3]);
+#endif
+  if (MK || CS) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {                                 // as stored
+      v[2 * q] = __uint_as_float(w[q] << 16);
+      v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  }
+  if (!MK) return 0u;
+  if (KIND == EPI_BDR && e.use_drop) return keep;
+  uint32_t pos = 0u;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) pos |= (uint32_t)(v[r] > 0.f) << r;
+  return pos;
+}
+
+// Accumulator image of the wide epilogue: [128][256] fp32, physical 16-B chunk = c ^ ((c >> 4) & 1) ^ (row & 15).
+// Fragment writes (8 consecutive rows per ds_write_b128 lane group, one chunk) and row-piece reads (lane l of a row
+// reads chunks 2l and 2l+1, one ds_read_b128 each) are both conflict-free, and each lane's two chunks arrive in
+// column order.
+VIT_DEV int v4w_chunk(int row, int c) { return c ^ ((c >> 4) & 1) ^ (row & 15); }
+
+template <int KIND, int ACT, bool MK, bool CS>
+VIT_DEV void v4_epilogue_w(const EpiParams& e, const f32x4 (&acc)[2][2][4][2], float* ep, int tid, int64_t i0,
+                           int64_t j0, int64_t tm) {
+  // ep: a [64][256] fp32 image (64 KiB, ring slots 4-7: the persistent kernel's next-tile stages fill slots 0-3
+  // meanwhile).  Pass k = tile rows [64k, 64k + 64): written by the 4 waves with wr == k & 1 (accumulator half
+  // mh = k >> 1), then read by all 8 waves, 8 rows = 4 row pairs each.
+  const int lane = tid & 63, l = lane & 31, hr = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t j = j0 + 8 * l;
+  const bool jok = j < e.n;                              // n % 8 == 0: a lane's 8 columns are all in or all out
+  float b8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias && jok) {
+    ld4<float>(e.bias + j, b8);
+    ld4<float>(e.bias + j + 4, b8 + 4);
+  }
+  const bool has_pre = v4_has_pre<KIND>(e);
+  // second-operand row pieces (pass k, pair p: row 64k + wave*8 + 2p + hr), one pass ahead of their use
+  uint4 pre[2][4];
+#define V4W_PRE(K)                                                                                  \
+  do {                                                                                              \
+    if (has_pre) {                                                                                  \
+      _Pragma("unroll") for (int p_ = 0; p_ < 4; ++p_) {                                            \
+        if (KIND != EPI_AUXM || (p_ & 1) == 0)                                                      \
+          pre[(K) & 1][p_] = v4_pre_load8<KIND>(e, i0 + 64 * (K) + wave * 8 + 2 * p_ + hr, j);       \
+        else                                                                                        \
+          pre[(K) & 1][p_] = pre[(K) & 1][p_ - 1];    /* rows 2p-2+hr, 2p+hr: one mask4 row group */ \
+      }                                                                                             \
+    }                                                                                               \
+  } while (0)
+  V4W_PRE(0);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  uint32_t mlo = 0u, mhi = 0u;                          // mask4 dwords of column groups 2l, 2l+1 being assembled
+  V4_LDS_BARRIER();                                     // every wave's k-loop reads of slots 4-7 are done
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < 3) V4W_PRE(k + 1);
+    if (wr == (k & 1)) {
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) {
+            const int row = x * 16 + (lane & 15);
+            const int chunk = (nh * 128 + wc * 32 + y * 16) / 4 + (lane >> 4);
+            *reinterpret_cast<f32x4*>(ep + row * 256 + (v4w_chunk(row, chunk) << 2)) = acc[k >> 1][nh][x][y];
+          }
+    }
+    V4_LDS_BARRIER();
+    f32x4 rv[4][2];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row = wave * 8 + 2 * p + hr;
+      rv[p][0] = *reinterpret_cast<const f32x4*>(ep + row * 256 + (v4w_chunk(row, 2 * l) << 2));
+      rv[p][1] = *reinterpret_cast<const f32x4*>(ep + row * 256 + (v4w_chunk(row, 2 * l + 1) << 2));
+    }
+    // uniform row base of this wave's 8 rows; per lane a 32-bit element offset
+    const int64_t rbase = i0 + 64 * k + wave * 8;
+    const int rows_left = (int)min((int64_t)8, max((int64_t)0, e.m - rbase));
+    bf16_t* cbase = (bf16_t*)e.c + rbase * e.ldc + j0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float v[8] = {rv[p][0][0], rv[p][0][1], rv[p][0][2], rv[p][0][3],
+                    rv[p][1][0], rv[p][1][1], rv[p][1][2], rv[p][1][3]};
+      const int rr = 2 * p + hr;
+      const int64_t i = rbase + rr;
+      const int sh = 8 * (rr & 3);
+      uint32_t bits = 0u;
+#ifdef VIT_GEMM_NOEPI
+      if (v[0] != 1234.5f) continue;
+#endif
+      if (jok && rr < rows_left) {
+        bf16_t* cp = cbase + (uint32_t)(rr * (int)e.ldc + 8 * l);
+        bits = v4_epi_row8<KIND, ACT, MK, CS>(e, i, j, cp, b8, v, has_pre ? pre[k & 1][p] : make_uint4(0u, 0u, 0u, 0u),
+                                             sh);
+        if (CS) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) cs[r] += v[r];
+        }
+      }
+      if (MK) {
+        mlo |= (bits & 0xfu) << sh;
+        mhi |= ((bits >> 4) & 0xfu) << sh;
+        if (p & 1) {
+          // rows 4q..4q+3 done: lane l (hr 0) holds bytes 0, 2 and lane l+32 bytes 1, 3 of both dwords; lane l
+          // stores column group 2l, lane l+32 column group 2l+1
+          const uint32_t recv = (uint32_t)__shfl_xor((int)(hr ? mlo : mhi), 32, 64);
+          if (2 * (p - 1) < rows_left && jok)
+            *reinterpret_cast<uint32_t*>(e.mask_out + mask4_byte(rbase + 2 * (p - 1), j + 4 * hr, e.n)) =
+                (hr ? mhi : mlo) | recv;
+          mlo = mhi = 0u;
+        }
+      }
+    }
+    V4_STAMP(3 + k);
+    if (k < 3) V4_LDS_BARRIER();                        // the next pass overwrites the image
+  }
+#undef V4W_PRE
+  if (CS) {
+    // even + odd rows of the wave, then the 8 wave sums in wave order through LDS: one row of csum per tile
+#pragma unroll
+    for (int r = 0; r < 8; ++r) cs[r] += __shfl_xor(cs[r], 32, 64);
+    V4_LDS_BARRIER();
+    if (hr == 0) {
+      *reinterpret_cast<f32x4*>(ep + wave * 256 + 8 * l) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      *reinterpret_cast<f32x4*>(ep + wave * 256 + 8 * l + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    }
+    V4_LDS_BARRIER();
+    if (tid < 256 && j0 + tid < e.n) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) sum += ep[w8 * 256 + tid];
+      e.csum[tm * e.n + j0 + tid] = sum;
+    }
+  }
+}
+
+// Direct wide epilogue (the persistent kernel's; no LDS image): in the 16x16 MFMA fragment a lane holds 4 consecutive
+// columns of one row in each of acc[..][y = 0] (columns 4q..4q+3 of the wave's 32-column slot, q = lane / 16) and
+// acc[..][y = 1] (16 + 4q..).  One v_permlane16_swap per register pair exchanges y = 1 of 16-lane row q = 0 (2) with
+// y = 0 of row q = 1 (3), after which every lane holds 8 consecutive columns, cq = 16 (q & 1) + 8 (q >> 1), of its row
+// and stores them as one 16-B piece; a store instruction covers 16 rows x 64 B.  No LDS round trip, no barriers, and
+// the whole LDS ring is free for the next tile's stages while this runs.
+VIT_DEV void swap16(f32x4& y0, f32x4& y1) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(y0[r]), __float_as_uint(y1[r]), false, false);
+    y0[r] = __uint_as_float(s[0]);
+    y1[r] = __uint_as_float(s[1]);
+  }
+}
+
+template <int KIND, int ACT, bool MK, bool CS>
+VIT_DEV void v4_epilogue_d(const EpiParams& e, f32x4 (&acc)[2][2][4][2], float* cs_lds, int tid, int64_t i0,
+                           int64_t j0, int64_t tm) {
+  const int lane = tid & 63, q = lane >> 4, r16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int cq = (q & 1) * 16 + (q >> 1) * 8;
+  float b8[2][8];
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) b8[nh][r] = 0.f;
+  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh) {
+      const int64_t j = j0 + nh * 128 + wc * 32 + cq;
+      if (j < e.n) {
+        ld4<float>(e.bias + j, b8[nh]);
+        ld4<float>(e.bias + j + 4, b8[nh] + 4);
+      }
+    }
+  }
+  const bool has_pre = v4_has_pre<KIND>(e);
+  float cs[2][8];
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) cs[nh][r] = 0.f;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+    const int64_t rbase = i0 + mh * 128 + wr * 64 + r16;       // + 16 x
+    uint4 pre[2][4];
+    if (has_pre) {
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) pre[nh][x] = v4_pre_load8<KIND>(e, rbase + 16 * x, j0 + nh * 128 + wc * 32 + cq);
+    }
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        f32x4 y0 = acc[mh][nh][x][0], y1 = acc[mh][nh][x][1];
+        swap16(y0, y1);
+        float v[8] = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+        const int64_t i = rbase + 16 * x, j = j0 + nh * 128 + wc * 32 + cq;
+        uint32_t bits = 0u;
+#ifdef VIT_GEMM_NOEPI
+        if (v[0] != 1234.5f) continue;
+#endif
+        if (i < e.m && j < e.n) {
+          bits = v4_epi_row8<KIND, ACT, MK, CS>(e, i, j, (bf16_t*)e.c + i * e.ldc + j, b8[nh], v,
+                                                has_pre ? pre[nh][x] : make_uint4(0u, 0u, 0u, 0u), 8 * (int)(i & 3));
+          if (CS) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) cs[nh][r] += v[r];
+          }
+        }
+        if (MK) {
+          // the 4 rows of a mask4 row group are the 4 lanes of a DPP quad: OR the bytes together, then the quad's
+          // first lane stores the dwords of column groups j/4 and j/4 + 1 (8 B)
+          int w = (int)(bits << (8 * (r16 & 3)));
+          w |= __builtin_amdgcn_mov_dpp(w, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+          w |= __builtin_amdgcn_mov_dpp(w, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+          if ((r16 & 3) == 0 && i < e.m && j < e.n) {
+            const uint32_t uw = (uint32_t)w;
+            *reinterpret_cast<uint2*>(e.mask_out + mask4_byte(i, j, e.n)) =
+                make_uint2(uw & 0x0f0f0f0fu, (uw >> 4) & 0x0f0f0f0fu);
+          }
+        }
+      }
+  }
+  if (CS) {
+    // the 16 rows of a 16-lane row -> lane r16 = 0 (fixed butterfly order), then the two row halves (wr) through LDS
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float t = cs[nh][r];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) t += __shfl_xor(t, o, 16);
+        cs[nh][r] = t;
+      }
+    if (r16 == 0) {
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+        float* d = cs_lds + wr * 256 + nh * 128 + wc * 32 + cq;
+        *reinterpret_cast<f32x4*>(d) = f32x4{cs[nh][0], cs[nh][1], cs[nh][2], cs[nh][3]};
+        *reinterpret_cast<f32x4*>(d + 4) = f32x4{cs[nh][4], cs[nh][5], cs[nh][6], cs[nh][7]};
+      }
+    }
+    V4_LDS_BARRIER();
+    if (tid < 256 && j0 + tid < e.n) e.csum[tm * e.n + j0 + tid] = cs_lds[tid] + cs_lds[256 + tid];
+  }
+}
+
+template <int KIND, int ACT>
+VIT_DEV void v4_epilogue_dd(const EpiParams& e, f32x4 (&acc)[2][2][4][2], float* cs_lds, int tid, int64_t i0,
+                            int64_t j0, int64_t tm) {
+  const bool mk = e.mask_out != nullptr, cs = e.csum != nullptr;
+  if (mk && cs) v4_epilogue_d<KIND, ACT, true, true>(e, acc, cs_lds, tid, i0, j0, tm);
+  else if (mk) v4_epilogue_d<KIND, ACT, true, false>(e, acc, cs_lds, tid, i0, j0, tm);
+  else if (cs) v4_epilogue_d<KIND, ACT, false, true>(e, acc, cs_lds, tid, i0, j0, tm);
+  else v4_epilogue_d<KIND, ACT, false, false>(e, acc, cs_lds, tid, i0, j0, tm);
+}
+
+// mask / column-sum switches of the wide epilogue as template arguments (no dead per-row work when off)
+template <int KIND, int ACT>
+VIT_DEV void v4_epilogue_wd(const EpiParams& e, const f32x4 (&acc)[2][2][4][2], float* ep, int tid, int64_t i0,
+                            int64_t j0, int64_t tm) {
+  const bool mk = e.mask_out != nullptr, cs = e.csum != nullptr;
+  if (mk && cs) v4_epilogue_w<KIND, ACT, true, true>(e, acc, ep, tid, i0, j0, tm);
+  else if (mk) v4_epilogue_w<KIND, ACT, true, false>(e, acc, ep, tid, i0, j0, tm);
+  else if (cs) v4_epilogue_w<KIND, ACT, false, true>(e, acc, ep, tid, i0, j0, tm);
+  else v4_epilogue_w<KIND, ACT, false, false>(e, acc, ep, tid, i0, j0, tm);
+}
+
+// Work item -> (tile row, tile column, K-slice).  Items are split-major (all tiles of K-slice 0, then slice 1, ...);
+// with group_m > 1 the tiles go in groups of group_m tile rows, column-major inside a group (L2 locality: the ~32
+// tiles an XCD runs at once span group_m A panels x 32/group_m B panels).
+VIT_DEV void v4_item(const GemmArgs& g, int64_t item, int64_t& tm, int64_t& tn, int64_t& sidx) {
   const int64_t ntile = g.tiles_m * g.tiles_n;
-  const int64_t sidx = bid_all / ntile, bid = bid_all % ntile;
-  int64_t tm, tn;
+  sidx = item / ntile;
+  const int64_t bid = item % ntile;
   if (g.group_m > 1) {
-    // L2 locality: the ~32 tiles an XCD runs at once span group_m A panels x 32/group_m B panels
     const int64_t span = g.group_m * g.tiles_n, first = (bid / span) * g.group_m;
     const int64_t gs = min(g.tiles_m - first, g.group_m), in = bid % span;
     tm = first + in % gs;
@@ -764,11 +1237,60 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     tm = bid / g.tiles_n;
     tn = bid % g.tiles_n;
   }
-  if (g.ws) g.ws += sidx * g.M * g.N;                  // this K-slice's fp32 slab (EPI_SLAB)
-  const int64_t i0 = tm * 256, j0 = tn * 256;
+}
+
+template <bool AKC, bool BKC>
+VIT_DEV void v4_offsets(const GemmArgs& g, int64_t i0, int64_t j0, int64_t k0, int wave, int lane, uint32_t (&oa0)[2],
+                        uint32_t (&oa1)[2], uint32_t (&ob0)[2], uint32_t (&ob1)[2]) {
+#ifdef V4_GLDS
+  dma_offsets4g<AKC>(g.lda, g.M, i0, k0, wave, lane, oa0);
+  dma_offsets4g<AKC>(g.lda, g.M, i0 + 128, k0, wave, lane, oa1);
+  dma_offsets4g<BKC>(g.ldb, g.N, j0, k0, wave, lane, ob0);
+  dma_offsets4g<BKC>(g.ldb, g.N, j0 + 128, k0, wave, lane, ob1);
+#else
+  dma_offsets4<AKC>(g.lda, g.M, i0, k0, wave, lane, oa0);
+  dma_offsets4<AKC>(g.lda, g.M, i0 + 128, k0, wave, lane, oa1);
+  dma_offsets4<BKC>(g.ldb, g.N, j0, k0, wave, lane, ob0);
+  dma_offsets4<BKC>(g.ldb, g.N, j0 + 128, k0, wave, lane, ob1);
+#endif
+}
+
+// Persistent form (the wide-epilogue kinds: bf16 output, fast epilogue; the host launches one workgroup per CU): a
+// workgroup loops over its items, and as soon as a tile's k-loop is done it issues the NEXT tile's first 4 stages
+// (LDS ring slots 0-3, whose last reads are behind the k-loop's final barrier) before running the epilogue on a
+// 64 KiB image in slots 4-7 — the next tile's pipeline fill overlaps the epilogue instead of following it
+// (tools/gemm_stamps.py: the fill was ~5.5k cycles of a ~50k-cycle K = 768 tile).  Other kinds (split-K slabs, fp32
+// or general epilogues) run one item per workgroup with the 128 KiB image, as before.
+template <bool AKC, bool BKC, class TO, int KIND>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, int64_t a_bytes, int64_t b_bytes) {
+  // the ring, then 2 KiB for the direct epilogue's column-sum combine
+  __shared__ __attribute__((aligned(16))) bf16_t smem4[V4_SLOTS * HALF + 1024];
+  constexpr bool WIDE = sizeof(TO) == 2 && KIND != EPI_GENERAL && KIND != EPI_SLAB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  // Workgroups are dealt round-robin over the 8 XCDs (linear id % 8).  Each XCD owns a contiguous range of items
+  // (bijective split of g.nitems into 8 parts), and its workgroups take items lo + local, lo + local + step, ...: the
+  // ~32 workgroups an XCD runs at once are consecutive items (tiles of ONE K-slice that share A row panels and B
+  // column panels), so the XCD's L2 serves the re-reads.  With one workgroup per item this is the previous bijective
+  // block remap.  (With the K-slices on gridDim.y the hardware's linear order x + y * gridDim.x scattered a panel's
+  // tiles over XCDs: the weight-gradient GEMMs fetched ~3.5x their operand bytes from beyond L2.)
+  const int64_t nwg = gridDim.x, orig = blockIdx.x;
+  const int64_t xcd = orig % 8, q8 = g.nitems / 8, r8 = g.nitems % 8;
+  const int64_t lo = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int64_t hi = lo + q8 + (xcd < r8 ? 1 : 0);
+  const int64_t step = (nwg - xcd + 7) / 8;              // workgroups on this XCD
+  int64_t item = lo + orig / 8;
+  if (item >= hi) return;
+#ifdef VIT_GEMM_STAMPS
+  unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last_ = __builtin_amdgcn_s_memtime();
+#endif
+  int64_t tm, tn, sidx;
+  v4_item(g, item, tm, tn, sidx);
+  int64_t i0 = tm * 256, j0 = tn * 256;
   const int64_t nkt = g.K / BK;
-  const int64_t kt0 = sidx * g.kt_per_split;
-  const int nk = (int)max((int64_t)0, min(nkt, kt0 + g.kt_per_split) - kt0);
+  int nk = (int)max((int64_t)0, min(nkt, (sidx + 1) * g.kt_per_split) - sidx * g.kt_per_split);
 #ifndef V4_GLDS
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
@@ -776,19 +1298,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
   const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
   uint32_t oa0[2], oa1[2], ob0[2], ob1[2];
+  v4_offsets<AKC, BKC>(g, i0, j0, sidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
 #ifdef V4_GLDS
-  dma_offsets4g<AKC>(g.lda, g.M, i0, kt0 * BK, wave, lane, oa0);
-  dma_offsets4g<AKC>(g.lda, g.M, i0 + 128, kt0 * BK, wave, lane, oa1);
-  dma_offsets4g<BKC>(g.ldb, g.N, j0, kt0 * BK, wave, lane, ob0);
-  dma_offsets4g<BKC>(g.ldb, g.N, j0 + 128, kt0 * BK, wave, lane, ob1);
   const char* pa_ = (const char*)g.a;
   const char* pb_ = (const char*)g.b;
 #define V4_DMA(R, P, OFF, SOFF, DST) dma_half_g(P, OFF, SOFF, DST, wave)
 #else
-  dma_offsets4<AKC>(g.lda, g.M, i0, kt0 * BK, wave, lane, oa0);
-  dma_offsets4<AKC>(g.lda, g.M, i0 + 128, kt0 * BK, wave, lane, oa1);
-  dma_offsets4<BKC>(g.ldb, g.N, j0, kt0 * BK, wave, lane, ob0);
-  dma_offsets4<BKC>(g.ldb, g.N, j0 + 128, kt0 * BK, wave, lane, ob1);
 #define V4_DMA(R, P, OFF, SOFF, DST) dma_half(R, OFF, SOFF, DST, wave)
 #endif
 
@@ -806,26 +1321,29 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     }                                                                                            \
   } while (0)
 
-  f32x4 acc[2][2][4][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) acc[a][b][x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nstage = 4 * nk;
-  // prologue: stages 0..LEAD-1; retire stages 0 and 1 (k-tile 0's A_0, B_0) before the common barrier
+  int nstage = 4 * nk;
+  // first item's prologue: stages 0..LEAD-1; retire stages 0 and 1 (k-tile 0's A_0, B_0) before the loop barrier
   for (int s = 0; s < V4_LEAD && s < nstage; ++s) V4_STAGE(s);
   if (nstage > 0) wait_stage_retired(min(V4_LEAD - 1, nstage - 1) - 1);
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();              // group 1 runs one barrier behind group 0
 
+  f32x4 acc[2][2][4][2];
   bf16x8_t af[4][2], b0f[2][2], b1f[2][2];
-  // One phase f = 4t + r.  STEADY: the k-tiles before the last two, where every phase issues its DMA stage and the
-  // retiring wait is the constant vmcnt(2 * (LEAD - 2)) — no per-phase branches (the tail's counts are computed).
+  V4_ACC(5);
+  while (true) {
+    __builtin_amdgcn_s_barrier();
+    V4_ACC(4);
+    if (wr == 1) __builtin_amdgcn_s_barrier();            // group 1 runs one barrier behind group 0
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) acc[a][b][x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // One phase f = 4t + r.  STEADY: the k-tiles before the last two, where every phase issues its DMA stage and the
+    // retiring wait is the constant vmcnt(2 * (LEAD - 2)) — no per-phase branches (the tail's counts are computed).
 #ifndef VIT_V4_NODMA
 #define V4_PHASE_DMA(F, STEADY)                                                                  \
   do {                                                                                           \
@@ -876,127 +1394,103 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     __builtin_amdgcn_s_barrier();                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                           \
   } while (0)
-  const int nsteady = nk > 2 ? nk - 2 : 0;            // LEAD in [4, 8]: phases of k-tiles < nk - 2 are steady
-  int t = 0;
-  for (; t < nsteady; ++t) {
-    V4_PHASE(t, 0, true);
-    V4_PHASE(t, 1, true);
-    V4_PHASE(t, 2, true);
-    V4_PHASE(t, 3, true);
-  }
-  for (; t < nk; ++t) {
-    V4_PHASE(t, 0, false);
-    V4_PHASE(t, 1, false);
-    V4_PHASE(t, 2, false);
-    V4_PHASE(t, 3, false);
-  }
+    const int nsteady = nk > 2 ? nk - 2 : 0;          // LEAD in [4, 8]: phases of k-tiles < nk - 2 are steady
+    int t = 0;
+    for (; t < nsteady; ++t) {
+      V4_PHASE(t, 0, true);
+      V4_PHASE(t, 1, true);
+      V4_PHASE(t, 2, true);
+      V4_PHASE(t, 3, true);
+    }
+    for (; t < nk; ++t) {
+      V4_PHASE(t, 0, false);
+      V4_PHASE(t, 1, false);
+      V4_PHASE(t, 2, false);
+      V4_PHASE(t, 3, false);
+    }
 #undef V4_PHASE
 #undef V4_PHASE_MFMA
 #undef V4_PHASE_DMA
-#undef V4_STAGE
-#undef V4_SLOT
-#undef V4_DMA
-  if (wr == 0) __builtin_amdgcn_s_barrier();              // balance group 1's extra barrier
+    if (wr == 0) __builtin_amdgcn_s_barrier();            // balance group 1's extra barrier
+    V4_ACC(0);
+
+    // next item: its first stages go out now (slots 0-3), ahead of this tile's epilogue
+    const int64_t next = item + step;
+    const bool have_next = WIDE && !(KIND == EPI_BIAS_ACT && e.act == VIT_ACT_GELU) && next < hi;
+    int64_t ni0 = 0, nj0 = 0, ntm = 0, ntn = 0, nsidx = 0;
+    int nnk = 0, npre = 0;
+    if (have_next) {
+      v4_item(g, next, ntm, ntn, nsidx);
+      ni0 = ntm * 256;
+      nj0 = ntn * 256;
+      nnk = (int)max((int64_t)0, min(nkt, (nsidx + 1) * g.kt_per_split) - nsidx * g.kt_per_split);
+      v4_offsets<AKC, BKC>(g, ni0, nj0, nsidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
+      npre = min(V4_LEAD, 4 * nnk);
+      for (int s = 0; s < npre; ++s) V4_STAGE(s);
+    }
+    V4_ACC(1);
 
 #if defined(VIT_V4_DIRECT_EPI)
 #pragma unroll
-  for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          const int64_t i = i0 + mh * 128 + wr * 64 + x * 16 + (lane & 15);
-          const int64_t j = j0 + nh * 128 + wc * 32 + y * 16 + 4 * (lane >> 4);
-          const f32x4 a = acc[mh][nh][x][y];
-          float v[4] = {a[0], a[1], a[2], a[3]};
-#ifdef VIT_GEMM_NOEPI
-          if (v[0] != 1234.5f) continue;
-#endif
-          v4_epi_row<TO, EPI_GENERAL>(e, g, i, j, v, false, false, v);
-        }
-#else
-  // Row-contiguous epilogue through LDS, one 128-row half of the tile per pass: the fragment layout (16 rows x 32 B
-  // per store instruction) becomes 1 row x 256 columns per wave instruction, so output stores and residual / mask
-  // loads are full-line.  Image: [128][256] fp32, 16-B chunk index XOR (row & 15) -> conflict-free b128 writes
-  // (8 rows per lane group) and reads (16 chunks of one row per group).
-  float* ep = reinterpret_cast<float*>(smem4);
-  const int64_t jcol = j0 + 4 * lane;
-  float b4[4] = {0.f, 0.f, 0.f, 0.f};
-  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias && jcol < e.n) ld4<float>(e.bias + jcol, b4);
-  const bool relu = e.act == VIT_ACT_RELU, gelu = e.act == VIT_ACT_GELU;
-  // second-operand rows of both passes, in flight before the LDS round trip (see v4_has_pre)
-  uint2 pre[2][16];
-  const bool has_pre = v4_has_pre<KIND>(e);
-  // fused column sums of C as stored (the bias gradient of the Linear whose input gradient C is)
-  const bool cs_on = (KIND == EPI_PLAIN || KIND == EPI_BIAS_ACT || KIND == EPI_AUX || KIND == EPI_AUXM ||
-                      KIND == EPI_BDR) && e.csum != nullptr;
-  // mask4 of C: 4 rows' nibbles of this lane's column group -> one dword store per 4 rows (EPI_GENERAL writes it in
-  // epilogue4, the split-K reduce after EPI_SLAB)
-  const bool mk_on = KIND != EPI_GENERAL && KIND != EPI_SLAB && e.mask_out != nullptr;
-  uint32_t mword = 0u;
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  if (has_pre) {
-#pragma unroll
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        if (KIND != EPI_AUXM) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
-        else if ((rr & 3) == 0) pre[mh][rr] = v4_pre_load<KIND>(e, i0 + mh * 128 + wave * 16 + rr, jcol);
-        else pre[mh][rr] = make_uint2(pre[mh][rr & ~3].x >> (8 * (rr & 3)), 0u);
-      }
-  }
-  __syncthreads();                                        // every wave's k-loop LDS reads are done, no DMA pending
+      for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-  for (int mh = 0; mh < 2; ++mh) {
+        for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          const int row = wr * 64 + x * 16 + (lane & 15);
-          const int chunk = (nh * 128 + wc * 32 + y * 16) / 4 + (lane >> 4);
-          *reinterpret_cast<f32x4*>(ep + row * 256 + ((chunk ^ (row & 15)) << 2)) = acc[mh][nh][x][y];
-        }
-    __syncthreads();
-#pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
-      const int row = wave * 16 + rr;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(ep + row * 256 + ((lane ^ (row & 15)) << 2));
-      float v[4] = {a[0], a[1], a[2], a[3]};
-      const int64_t i = i0 + mh * 128 + row, j = j0 + 4 * lane;
-#ifdef VIT_GEMM_NOEPI
-      if (v[0] != 1234.5f) continue;
+          for (int y = 0; y < 2; ++y) {
+            const int64_t i = i0 + mh * 128 + wr * 64 + x * 16 + (lane & 15);
+            const int64_t j = j0 + nh * 128 + wc * 32 + y * 16 + 4 * (lane >> 4);
+            const f32x4 a = acc[mh][nh][x][y];
+            float v[4] = {a[0], a[1], a[2], a[3]};
+            v4_epi_row<TO, EPI_GENERAL, 0>(e, g, i, j, v, v);
+          }
+#else
+    // The epilogue's per-lane address arithmetic is loop-invariant; hoisted out of the persistent loop it stayed live
+    // across the k-loop and spilled.  An opaque copy of tid makes the compiler recompute it per tile (a few dozen VALU).
+    int tid_e = tid;
+    asm volatile("" : "+v"(tid_e));
+    if constexpr (WIDE) {
+      float* csl = reinterpret_cast<float*>(smem4 + V4_SLOTS * HALF);
+      if (KIND == EPI_BIAS_ACT && e.act == VIT_ACT_RELU) v4_epilogue_dd<KIND, 1>(e, acc, csl, tid_e, i0, j0, tm);
+      else if (KIND == EPI_BIAS_ACT && e.act == VIT_ACT_GELU) {  // (the head only; erf x 8 per piece spills)
+        __syncthreads();
+        v4_epilogue<TO, KIND, 2>(e, g, acc, smem4, tid_e, i0, j0, tm);
+      } else v4_epilogue_dd<KIND, 0>(e, acc, csl, tid_e, i0, j0, tm);
+    } else {
+      GemmArgs gi = g;
+      if (gi.ws) gi.ws += sidx * g.M * g.N;                 // this K-slice's fp32 slab (EPI_SLAB)
+      v4_epilogue<TO, KIND, 0>(e, gi, acc, smem4, tid_e, i0, j0, tm);
+    }
 #endif
-      const uint32_t nib = v4_epi_row<TO, KIND>(e, g, i, j, b4, relu, gelu, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
-      if (mk_on) {
-        mword |= (nib & 0xfu) << (8 * (rr & 3));
-        if ((rr & 3) == 3) {                            // rows i-3..i: one dword (row groups are allocated whole)
-          if (i - 3 < e.m && j < e.n)
-            *reinterpret_cast<uint32_t*>(e.mask_out + mask4_byte(i - 3, j, e.n)) = mword;
-          mword = 0u;
-        }
-      }
-      if (cs_on && i < e.m) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cs[r] += sizeof(TO) == 2 ? bf2f(f2bf(v[r])) : v[r];
-      }
-    }
-    if (mh == 0) __syncthreads();
+    V4_ACC(2);
+#ifdef VIT_GEMM_STAMPS
+    st_acc_[6] += 1;
+#endif
+    if (!have_next) break;
+    // advance: the rest of the next item's prologue (its stages 4..LEAD-1 land in slots the image used)
+    item = next;
+    i0 = ni0;
+    j0 = nj0;
+    tm = ntm;
+    nk = nnk;
+    nstage = 4 * nk;
+    // the offsets again (recomputed rather than kept live across the epilogue: register budget)
+    v4_offsets<AKC, BKC>(g, i0, j0, nsidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
+    // stages 0..LEAD-1 went out before the epilogue; its loads and stores are younger, so retiring stages 0 and 1
+    // waits for them too (vmcnt counts in order): wait for everything
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    V4_ACC(3);
   }
-  if (cs_on) {
-    // per-lane sums of the wave's 32 rows -> LDS -> the 8 wave sums added in wave order: one row of csum per tile
-    __syncthreads();
-    *reinterpret_cast<f32x4*>(ep + wave * 256 + 4 * lane) = f32x4{cs[0], cs[1], cs[2], cs[3]};
-    __syncthreads();
-    if (tid < 256 && j0 + tid < e.n) {
-      float sum = 0.f;
+#undef V4_STAGE
+#undef V4_SLOT
+#undef V4_DMA
+#ifdef VIT_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  V4_ACC(7);
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {
 #pragma unroll
-      for (int w8 = 0; w8 < 8; ++w8) sum += ep[w8 * 256 + tid];
-      e.csum[tm * e.n + j0 + tid] = sum;
-    }
+    for (int k = 0; k < 8; ++k) vit_stamps[blockIdx.x * 8 + k] = st_acc_[k];
   }
 #endif
 }
@@ -1127,6 +1621,17 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
 
 }  // namespace
 
+#ifdef VIT_GEMM_STAMPS
+extern "C" int vit_gemm_debug_stamps(void* dst, int64_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(vit_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int vit_gemm_debug_stamps_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(vit_stamps)) != hipSuccess) return 1;
+  return (int)hipMemset(p, 0, sizeof(unsigned long long) * 16384 * 8);
+}
+#endif
+
 extern "C" int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d) {
   if (!d) return 0;
   if (d->split_k > 1) return (int64_t)d->split_k * d->m * d->n * (int64_t)sizeof(float);
@@ -1192,6 +1697,10 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
   e.vec = (d->n % 4 == 0) && (d->ldc % 4 == 0) && aligned(d->c, 16) && aligned(d->bias, 16) &&
           (!d->aux || d->aux_dtype == VIT_MASK4 || (d->ldaux % 4 == 0 && aligned(d->aux, 16))) &&
           (!d->res || (d->ldres % 4 == 0 && aligned(d->res, 16)));
+  e.vec8 = e.vec && d->n % 8 == 0 && d->ldc % 8 == 0 &&
+           (!d->aux || d->aux_dtype == VIT_MASK4 || (d->ldaux % 8 == 0 && aligned(d->aux, 16))) &&
+           (!d->res || (d->ldres % 8 == 0 && aligned(d->res, 16))) && (!d->mask_out || aligned(d->mask_out, 8)) &&
+           (!d->aux || d->aux_dtype != VIT_MASK4 || aligned(d->aux, 8));
 
   GemmArgs g{};
   g.a = d->a; g.b = d->b; g.lda = d->lda; g.ldb = d->ldb; g.M = d->m; g.N = d->n; g.K = d->k;
@@ -1236,7 +1745,8 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
       if (g4.group_m < 1) g4.group_m = 1;
     }
     g4.kt_per_split = (nkt + split - 1) / split;
-    dim3 grid4((unsigned)(((d->m + 255) / 256) * g4.tiles_n * split), 1u);   // tiles x K-slices, split-major
+    g4.nitems = ((d->m + 255) / 256) * g4.tiles_n * split;     // tiles x K-slices, split-major
+    dim3 grid4((unsigned)g4.nitems, 1u);
     // v4 epilogue kind
     const bool fast = e.vec && e.grp == 0 && e.res_rowmod == 0 && e.beta == 0.f;
     int kind = EPI_GENERAL;
@@ -1258,7 +1768,16 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     else if (out_bf && akc && bkc && (kind == EPI_BIAS_ACT || kind == EPI_BDR)) launched = kind;
     else if (out_bf && akc && !bkc && kind == EPI_AUX) launched = EPI_AUX;
     else if (out_bf && akc && !bkc && kind == EPI_AUXM) launched = EPI_AUXM;
+    if (launched != EPI_SLAB && launched != EPI_GENERAL && !e.vec8) launched = EPI_GENERAL;  // wide epilogue needs 8-wide rows
     cs_fused = v4 && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
+    // persistent grid (one workgroup per CU looping over items) for the wide-epilogue kinds; VIT_GEMM_PERSIST=0: one
+    // workgroup per item (A/B switch)
+    {
+      const char* pv = getenv("VIT_GEMM_PERSIST");
+      const bool persist = launched != EPI_SLAB && launched != EPI_GENERAL && e.act != VIT_ACT_GELU &&
+                           !(pv && pv[0] == '0');
+      if (persist && g4.nitems > vit_cu_count()) grid4.x = (unsigned)vit_cu_count();
+    }
     e.csum = cs_fused ? d->colsum_part : nullptr;
 #define V4(AK, BKK, TO, KIND) gemm_bf16_v4<AK, BKK, TO, KIND><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes)
 #define LAUNCH_BF(AK, BKK)                                                                                     \
