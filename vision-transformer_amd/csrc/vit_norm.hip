@@ -238,9 +238,131 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
     for (int s = 0; s < nset; ++s) partial[(s * parts + blockIdx.x) * cols + c] = s == 2 ? red[s][c] * oscale : red[s][c];
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// bf16, 16 B per lane: a wave takes two rows at once (lanes 0-31 row 2p, lanes 32-63 row 2p + 1), each lane 8
+// consecutive columns of every 256-column piece, so every load and store instruction moves 1 KiB (the 8-B-per-lane
+// form moved 512 B and held both LayerNorm kernels near 3.5-3.9 TB/s).  Row statistics are half-wave reductions.
+// Waves loop over row pairs with the next pair's operands in flight.  Used when cols and every row stride are
+// multiples of 8 (16-B aligned rows); the kernels above cover the rest and fp32.  Measured (tools/ln_bench.py,
+// 50432 x 768): 39-41 -> 38 us.  The same layout for the backward (and a 64-lane form with 16-B pairs of quads) was
+// slower than ln_bwd_kernel (97-120 vs 82-102 us): its per-lane accumulators cost occupancy.
+// ---------------------------------------------------------------------------------------------------------------
+VIT_DEV float half_sum(float v) {          // sum over the 32 lanes of this half-wave
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+VIT_DEV void unpack8(uint4 u, float (&a)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[2 * q] = __uint_as_float(w[q] << 16);
+    a[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+
+VIT_DEV uint4 pack8(const float (&v)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+VIT_DEV void ld8f(const float* p, float (&v)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd16_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ mean,
+                                                       float* __restrict__ rstd, int64_t rows, int64_t cols, float eps) {
+  const int lane = threadIdx.x & 63, l = lane & 31, hr = lane >> 5;
+  const int64_t npairs = (rows + 1) >> 1, stride = (int64_t)gridDim.x * 4;
+  int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= npairs) return;
+  uint4 nx[NV];
+  auto load = [&](int64_t pp) {
+    const int64_t row = 2 * pp + hr;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t c = (int64_t)k * 256 + 8 * l;
+      nx[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (row < rows && c < cols) nx[k] = *reinterpret_cast<const uint4*>(x + row * ldx + c);
+    }
+  };
+  load(p);
+  for (; p < npairs; p += stride) {
+    float v[NV][8];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) unpack8(nx[k], v[k]);
+    if (p + stride < npairs) load(p + stride);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s += v[k][r];
+    const float mu = half_sum(s) / (float)cols;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      if ((int64_t)k * 256 + 8 * l < cols) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float d = v[k][r] - mu;
+          q += d * d;
+        }
+      }
+    }
+    const float rs = rsqrtf(half_sum(q) / (float)cols + eps);
+    const int64_t row = 2 * p + hr;
+    if (row < rows) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t c = (int64_t)k * 256 + 8 * l;
+        if (c < cols) {
+          float g[8], b[8], o[8];
+          ld8f(gamma + c, g);
+          ld8f(beta + c, b);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = (v[k][r] - mu) * rs * g[r] + b[r];
+          *reinterpret_cast<uint4*>(y + row * ldy + c) = pack8(o);
+        }
+      }
+      if (l == 0) {
+        mean[row] = mu;
+        rstd[row] = rs;
+      }
+    }
+  }
+}
+
+// the 16-B forward applies: bf16, cols and every row stride multiples of 8, 16-B aligned base pointers
+static bool ln16_ok(int64_t cols, std::initializer_list<int64_t> lds, std::initializer_list<const void*> ptrs) {
+  static const bool on = [] { const char* e = getenv("VIT_LN16"); return !e || atoi(e) != 0; }();
+  if (!on || cols % 8) return false;
+  for (int64_t ld : lds)
+    if (ld % 8) return false;
+  for (const void* p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) % 16) return false;
+  return true;
+}
+
 template <int NV, class T>
 int ln_fwd_launch(const T* x, int64_t ldx, const float* g, const float* b, T* y, int64_t ldy, float* mean,
                   float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (ln16_ok(cols, {ldx, ldy}, {x, y})) {
+      // pairs of rows, 4 per block; enough blocks for 8 waves per SIMD, each wave looping over its pairs
+      const int64_t blocks = ((rows + 1) / 2 + 3) / 4;
+      const unsigned grid = (unsigned)std::min<int64_t>(blocks, vit_cu_count() * 8);
+      ln_fwd16_kernel<NV><<<grid, 256, 0, s>>>(x, ldx, g, b, y, ldy, mean, rstd, rows, cols, eps);
+      return 0;
+    }
+  }
   const unsigned grid = (unsigned)((rows + 3) / 4);
   ln_fwd_kernel<T, NV><<<grid, 256, 0, s>>>(x, ldx, g, b, y, ldy, mean, rstd, rows, cols, eps);
   return 0;
