@@ -1608,8 +1608,10 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
   const int64_t tn = (d->n + 255) / 256, tm = (d->m + 255) / 256, nkt = d->k / BK;
   const int64_t rounds = tm * tn / 256;
   // measured (ViT-B/16 B=256, N = 768): a net win at K >= 2304, a loss at K = 768, where a tile's k-loop is short
-  // against the slab round trip
-  if (rounds < 1 || nkt < 32) return 1;
+  // against the slab round trip.  Re-measured with the persistent kernel (tools/bench_ab.sh, whole step): the tail
+  // saves 0.45 ms/step; extending it to K = 768 (VIT_GEMM_TAIL_MINKT=8: proj, fc1, dgrad fc2 / proj) costs 1.0 ms.
+  static const int64_t min_kt = [] { const char* e = getenv("VIT_GEMM_TAIL_MINKT"); return e ? atoll(e) : 32; }();
+  if (rounds < 1 || nkt < min_kt) return 1;
   const int64_t mr = rounds * 256 / tn;                    // tile rows that fill whole rounds
   const int64_t tail = (tm - mr) * tn;                     // tiles of the last, partial round
   if (tail <= 0 || 2 * tail > 256) return 1;
