@@ -51,9 +51,13 @@ def _hd64_cfg(img=64, batch=3, blocks=2):
     return ocfg
 
 
+@pytest.mark.parametrize("preset,img", [("base", 224), ("large", 224), ("base", 384)],
+                         ids=["C2_base224", "C4_large224", "C5_base384"])
 @pytest.mark.parametrize("train", [False, True])
-def test_base_width_bf16_engine_vs_oracle(train):
-    """C2 shapes through the engine in bf16: D=768, H=12 (hd 64), T=197 (224^2 / 16), L=2, B=2, nc=1000.
+def test_base_width_bf16_engine_vs_oracle(train, preset, img):
+    """BASELINE shapes through the engine in bf16 at L=2, B=2, nc=1000: C2 (D=768, H=12, hd 64, T=197), C4's ViT-L
+    width (D=1024, H=16, T=197: v4 GEMMs at N=1024/3072/4096, split-K wgrad at D=1024) and C5's sequence (T=577 at
+    D=768: the tiled T > 256 attention kernels and v4 GEMMs at M=1154).
 
     Tolerance scale: the spread of VALID bf16 evaluations, each rounding to bf16 at this path's storage points —
     the oracle with fp32 arithmetic between them, the same with fp64, and the same with the MFMA flash-attention
@@ -66,7 +70,7 @@ def test_base_width_bf16_engine_vs_oracle(train):
         classifier reads token 0), and two valid evaluations differ by 10-200% on single heads (measured);
       * the whole gradient vector: <= max(1e-2, 2 x the largest valid error).
     Train mode uses the same counter-hash dropout masks in all evaluations (element-exact mask parity)."""
-    ocfg = O.make_config("base", img=224, batch=2, blocks=2, num_classes=1000)
+    ocfg = O.make_config(preset, img=img, batch=2, blocks=2, num_classes=1000)
     st = O.init_state(ocfg, seed=21)
     m = _model(ocfg, st, torch.bfloat16).train(train)
     x, y = O.synthetic_batch(ocfg)

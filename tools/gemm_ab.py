@@ -25,6 +25,9 @@ SHAPES = {  # name: m, n, k, a_kcontig, b_kcontig, epilogue
     "wgrad_fc1": (4 * D, D, M, False, False, "wgrad"), "wgrad_fc2": (D, 4 * D, M, False, False, "wgrad"),
     "wgrad_qkv": (3 * D, D, M, False, False, "wgrad"), "wgrad_proj": (D, D, M, False, False, "wgrad"),
     "sq8192": (8192, 8192, 8192, True, True, None),
+    # the same square GEMM in the dgrad (A k-contiguous, B row-strided) and weight-gradient (both row-strided, f32 out)
+    # operand layouts: what the transposed LDS reads cost the k-loop
+    "sq8192_kr": (8192, 8192, 8192, True, False, None), "sq8192_rr": (8192, 8192, 8192, False, False, "wgrad"),
     # one-round grids (epilogue cost vs how many CUs store at once)
     "fc1m_t24": (512, 4 * D, D, True, True, "bias_relu_m"), "fc1m_t96": (2048, 4 * D, D, True, True, "bias_relu_m"),
     "fc1m_t252": (5376, 4 * D, D, True, True, "bias_relu_m"), "fc1m_t504": (10752, 4 * D, D, True, True, "bias_relu_m"),
