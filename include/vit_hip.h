@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 7
+#define VIT_ABI_VERSION 8
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -31,6 +31,14 @@ typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
  * ((i/4)*ceil(n/4) + j/4)*4 + i%4, bit j%4; 4*ceil(m/4)*ceil(n/4) bytes.  One byte = 4 columns of a row; one dword =
  * a 4 x 4 block (byte = row).  8x smaller than the bf16 tensor it replaces as a mask source. */
 typedef enum { VIT_ACT_NONE = 0, VIT_ACT_RELU = 1, VIT_ACT_GELU = 2 } vit_act;
+
+/* Launch flags (vit_gemm_desc.flags, vit_attn_bwd `flags`).
+ * VIT_FLAG_SHARED_CUS: other kernels may hold compute units while this launch runs — RCCL all-reduce kernels of the
+ *   data-parallel backward overlap it.  Kernels that otherwise run a persistent one-workgroup-per-CU grid with a
+ *   static item assignment (the bf16 GEMM's wide-epilogue kinds, the fused attention backward) then launch one
+ *   workgroup per item, so the hardware places work on whichever CUs are free instead of a workgroup waiting for a
+ *   CU a collective holds.  Same arithmetic, bitwise-identical results. */
+#define VIT_FLAG_SHARED_CUS 1
 
 int vit_abi_version(void);
 const char* vit_last_error(void);
@@ -81,6 +89,7 @@ typedef struct vit_gemm_desc {
   /* 0/1, or S: the dropout index of output row i is (i * S) * n + j — C computes rows i*S of a larger [m*S][n] tensor
    * (the last block's token-0 rows, ldA = S*K), and its dropout draws the same bits as the full tensor's rows. */
   int64_t dropout_row_stride;
+  int32_t flags;      /* VIT_FLAG_* */
 } vit_gemm_desc;
 
 /* Workspace vit_gemm can use: split_k > 1: the K-split fp32 slabs (required).  split_k <= 1: the slabs of the split-K
@@ -149,7 +158,7 @@ int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, float* probs,
 int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
 int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d_o, const float* lse, void* dqkv,
                  int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace,
-                 void* stream);
+                 int32_t flags, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------
  * Reductions / elementwise.

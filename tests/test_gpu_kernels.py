@@ -357,27 +357,29 @@ def test_gemm_persistent_matches_one_per_item(monkeypatch, variant):
     res = _ints((M, N), gen=g)
     mask_in = torch.randint(0, 256, (_ops.mask4_bytes(M, N),), generator=g, dtype=torch.uint8).to(DEV)
     results = []
-    for persist in ("1", "0"):
-        monkeypatch.setenv("VIT_GEMM_PERSIST", persist)
+    for persist in ("1", "0", "shared"):      # "shared": VIT_FLAG_SHARED_CUS (the data-parallel backward's launches)
+        monkeypatch.setenv("VIT_GEMM_PERSIST", "0" if persist == "0" else "1")
+        sh = dict(shared_cus=persist == "shared")
         c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         part = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
         mask = torch.full((_ops.mask4_bytes(M, N),), 0xAA, dtype=torch.uint8, device=DEV)
         if variant in ("aux_cs", "auxm_cs"):             # dgrad layout (B row-strided), ReLU-backward mask
             bt = b.t().contiguous()
             kw = dict(aux=aux, ldaux=N) if variant == "aux_cs" else dict(aux=mask_in)
-            _ops.gemm(a, bt, c, M, N, K, K, N, N, b_kcontig=False, colsum_part=part, alpha=0.5, **kw)
+            _ops.gemm(a, bt, c, M, N, K, K, N, N, b_kcontig=False, colsum_part=part, alpha=0.5, **kw, **sh)
         else:
             kw = {"plain_cs": dict(colsum_part=part), "bias_relu_mask": dict(bias=bias, act=_ops.ACT_RELU, mask_out=mask),
                   "bias_drop_res_mask": dict(bias=bias, dropout_p=0.2, seed=5, res=res, ldres=N, mask_out=mask)}.get(
                       variant, {})
-            _ops.gemm(a, b, c, M, N, K, K, K, N, **kw)
+            _ops.gemm(a, b, c, M, N, K, K, K, N, **kw, **sh)
         results.append((c, part if "cs" in variant else None, mask if "mask" in variant else None))
-    (c1, p1, m1), (c0, p0, m0) = results
-    assert torch.equal(c1, c0)
-    if p1 is not None:
-        assert torch.equal(p1, p0)
-    if m1 is not None:
-        assert torch.equal(m1, m0)
+    (c1, p1, m1) = results[0]
+    for c0, p0, m0 in results[1:]:
+        assert torch.equal(c1, c0)
+        if p1 is not None:
+            assert torch.equal(p1, p0)
+        if m1 is not None:
+            assert torch.equal(m1, m0)
     if variant in ("plain", "grouped"):
         assert torch.equal(c1, (a.double() @ b.double().t()).float().bfloat16())
 
@@ -437,6 +439,22 @@ def test_attention_bwd_fused_matches_split(monkeypatch, T):
     es = (split.double() - g).abs().max().item()
     assert ef <= max(2 * es, 1e-2 * max(1.0, g.abs().max().item())), (ef, es)
     assert (fused.float() - split.float()).abs().max().item() <= 2e-2 * max(1.0, g.abs().max().item())
+
+
+@pytest.mark.parametrize("o32", [False, True])
+def test_attention_bwd_shared_cus_bitwise(o32):
+    """VIT_FLAG_SHARED_CUS (one workgroup per (image, head) instead of the persistent one-per-CU grid that stages the
+    next item during the current one): bitwise the same dQ / dK / dV, with more items than CUs."""
+    torch.manual_seed(3)
+    B, H, hd, T = 24, 12, 64, 197                       # 288 items
+    D = H * hd
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).bfloat16()
+    o32_t = torch.empty(B * T, D, device=DEV) if o32 else None
+    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0, o32=o32_t)
+    d_o = torch.randn(B * T, D, device=DEV).bfloat16()
+    a = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, o32=o32_t)
+    b = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, o32=o32_t, shared_cus=True)
+    assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("T", [1, 31, 32, 33, 197, 256])

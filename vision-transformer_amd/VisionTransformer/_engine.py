@@ -120,6 +120,8 @@ class Engine:
         # weight-gradient GEMMs on a side stream (VIT_CONCURRENT_WGRAD=1).  Off by default: measured on ViT-B/16
         # B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms/step).
         self.concurrent_wgrad = os.environ.get("VIT_CONCURRENT_WGRAD", "0") == "1"
+        # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend)
+        self.shared_cus = self.env_shared_cus(False)
         self._wstream = None
         self._wws = None
 
@@ -290,6 +292,12 @@ class Engine:
             self._wstream = torch.cuda.Stream(device=self.device)
         return self._wstream
 
+    @staticmethod
+    def env_shared_cus(default):
+        """VIT_SHARED_CUS=0/1 overrides the launch mode of the backward's persistent kernels (A/B runs)."""
+        v = os.environ.get("VIT_SHARED_CUS")
+        return default if v is None else v == "1"
+
     def _mark(self, fam, phase, flop=0.0, nbytes=0.0):
         h = self.profile_hook
         if h is not None:
@@ -327,6 +335,10 @@ class Engine:
         if split > 1:
             kw.update(split_k=split, workspace=self._workspace(split * m * n * 4))
         return _ops.gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw)
+
+    def _gemm_bwd(self, *args, **kw):
+        """A backward GEMM that may overlap the bucket all-reduce (launch mode: self.shared_cus)."""
+        return _ops.gemm(*args, shared_cus=self.shared_cus, **kw)
 
     def _head_gemm(self, a, b, c, m, n, k, lda, ldb, ldc, **kw):
         split = head_split_for(m, n, k)
@@ -580,14 +592,15 @@ class Engine:
             # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
             mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + R * D // 2)
             self._gemm_rows(pr, g1, self.ww[f"{l}.fc2_w"], dh, R, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
-                            colsum_part=dh_part, alpha=gs)
+                            colsum_part=dh_part, alpha=gs, shared_cus=self.shared_cus)
             mk("gemm_dgrad", 1)
             _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
             if req[f"{l}.fc1_w"]:
                 self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, R, 4 * D, D, beta, side, "gemm_wgrad")
             da2 = torch.empty(R, D, dtype=dt, device=dev)
             mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + R * D) * es)
-            self._gemm_rows(pr, dh, self.ww[f"{l}.fc1_w"], da2, R, D, 4 * D, 4 * D, D, D, b_kcontig=False)
+            self._gemm_rows(pr, dh, self.ww[f"{l}.fc1_w"], da2, R, D, 4 * D, 4 * D, D, D, b_kcontig=False,
+                            shared_cus=self.shared_cus)
             mk("gemm_dgrad", 1)
             dx_mid = torch.empty(R, D, dtype=dt, device=dev)
             g0 = torch.empty(R, D, dtype=dt, device=dev) if tape.training else None
@@ -605,7 +618,8 @@ class Engine:
                 self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, R, D, rs * D, beta, side, "gemm_wgrad", alpha=gs)
             do = torch.empty(R, D, dtype=dt, device=dev)
             mk("gemm_dgrad", 0, 2.0 * R * D * D, (2 * R * D + D * D) * es)
-            self._gemm_rows(pr, g0, self.ww[f"{l}.proj_w"], do, R, D, D, D, D, D, b_kcontig=False, alpha=gs)
+            self._gemm_rows(pr, g0, self.ww[f"{l}.proj_w"], do, R, D, D, D, D, D, b_kcontig=False, alpha=gs,
+                            shared_cus=self.shared_cus)
             mk("gemm_dgrad", 1)
             if pr:
                 # back to all M rows for the attention backward (zero outside the token-0 rows)
@@ -617,13 +631,14 @@ class Engine:
             mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 8 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                           else 0))
             dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
-                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32)
+                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32,
+                                 shared_cus=self.shared_cus)
             mk("attn_bwd", 1)
             if req[f"{l}.qkv_w"]:
                 self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
             da1 = torch.empty(M, D, dtype=dt, device=dev)
             mk("gemm_dgrad", 0, 2.0 * M * 3 * D * D, (3 * M * D + 3 * D * D + M * D) * es)
-            _ops.gemm(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
+            self._gemm_bwd(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
             mk("gemm_dgrad", 1)
             dx_in = torch.empty(M, D, dtype=dt, device=dev)
             g1n = torch.empty(M, D, dtype=dt, device=dev) if (tape.training and l > 0) else None

@@ -10,9 +10,10 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 F32, BF16, MASK4 = 0, 1, 2
+FLAG_SHARED_CUS = 1          # VIT_FLAG_SHARED_CUS (vit_hip.h)
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 
 
@@ -36,6 +37,7 @@ class GemmDesc(ctypes.Structure):
         ("colsum_part", ctypes.c_void_p),
         ("mask_out", ctypes.c_void_p),
         ("dropout_row_stride", ctypes.c_int64),
+        ("flags", ctypes.c_int32),
     ]
 
 
@@ -62,7 +64,7 @@ _SIGS = {
                                          _I64, _I32, _P]),
     "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
-    "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _P]),
+    "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _I32, _P]),
     "vit_colsum_workspace_bytes": (_I64, [_I64, _I64]),
     "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _F, _P, _P]),
     "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),

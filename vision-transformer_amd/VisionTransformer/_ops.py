@@ -5,7 +5,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, MASK4  # noqa: F401
+from ._lib import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, FLAG_SHARED_CUS, MASK4  # noqa: F401
 
 _DT = {torch.float32: F32, torch.bfloat16: BF16}
 
@@ -44,8 +44,10 @@ def mask4_empty(m, n, device):
 
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=1.0, beta=0.0, bias=None,
          act=ACT_NONE, aux=None, ldaux=0, res=None, ldres=0, res_rowmod=0, dropout_p=0.0, seed=0, split_k=1,
-         out_group=(0, 0), workspace=None, colsum_part=None, mask_out=None, drop_row_stride=1, stream=None):
-    """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  `colsum_part` (f32, colsum_part_rows(m) x n)
+         out_group=(0, 0), workspace=None, colsum_part=None, mask_out=None, drop_row_stride=1, shared_cus=False,
+         stream=None):
+    """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  `shared_cus`: VIT_FLAG_SHARED_CUS (other
+    kernels — RCCL collectives — may hold CUs meanwhile: no persistent grid).  `colsum_part` (f32, colsum_part_rows(m) x n)
     receives per-256-row-block column sums of C as stored — finish with colsum_finish.  `aux` may be a uint8 mask4
     tensor (the ReLU mask saved by the forward); `mask_out` (uint8, mask4_bytes(m, n)) receives C's mask4 (dropout
     keep bits when dropout_p > 0, else C > 0).  `drop_row_stride` S: output row i draws the dropout bits of row i*S of
@@ -76,6 +78,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=
             raise ValueError("gemm: mask_out must be uint8 with >= mask4_bytes(m, n) elements")
         d.mask_out = mask_out.data_ptr()
     d.dropout_row_stride = drop_row_stride
+    d.flags = FLAG_SHARED_CUS if shared_cus else 0
     if res is not None:
         d.res, d.ldres, d.res_rowmod, d.res_dtype = res.data_ptr(), ldres, res_rowmod, dtype_code(res)
     d.dropout_p, d.dropout_seed = dropout_p, seed & 0xFFFFFFFF
@@ -180,13 +183,14 @@ def attn_bwd_workspace_bytes(B, T, H, hd, dtype):
     return _lib.load().vit_attn_bwd_workspace_bytes(B, T, H, hd, dtype_code(dtype))
 
 
-def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, o32=None, stream=None):
+def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, o32=None, shared_cus=False,
+             stream=None):
     dqkv = torch.empty_like(qkv) if dqkv is None else dqkv
     need = attn_bwd_workspace_bytes(B, T, H, hd, qkv.dtype)
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty(max(need // 4, 1), dtype=torch.float32, device=qkv.device)
     _lib.call("vit_attn_bwd", _ptr(qkv), _ptr(o), _ptr(o32), _ptr(d_o), _ptr(lse), _ptr(dqkv), B, T, H, hd, scale,
-              dtype_code(qkv), _ptr(workspace), _stream(stream))
+              dtype_code(qkv), _ptr(workspace), FLAG_SHARED_CUS if shared_cus else 0, _stream(stream))
     return dqkv
 
 

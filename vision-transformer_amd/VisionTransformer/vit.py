@@ -104,6 +104,9 @@ class VisionTransformer(nn.Module):
         eng = self.hip_engine
         eng.ddp_group = group
         eng.ddp_enabled = bool(force) or dist.get_world_size(group) > 1
+        # RCCL's all-reduce kernels run on the GPU beside the backward: the backward's kernels then launch one
+        # workgroup per item instead of a persistent one-per-CU grid (VIT_FLAG_SHARED_CUS, vit_hip.h)
+        eng.shared_cus = eng.env_shared_cus(eng.ddp_enabled and dist.get_backend(group) == "nccl")
         return self
 
     # the engine holds a weakref to its model and views of the parameters: never copy or pickle it (a deep copy or

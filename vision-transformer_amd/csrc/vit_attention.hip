@@ -1083,7 +1083,7 @@ extern "C" int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H,
 
 extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d_o, const float* lse,
                             void* dqkv, int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype,
-                            void* workspace, void* stream) {
+                            void* workspace, int32_t flags, void* stream) {
   VIT_REQUIRE(qkv && o && d_o && lse && dqkv && workspace && B > 0 && T > 0 && H > 0 && hd > 0,
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
@@ -1097,7 +1097,8 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
       attn_delta<float><<<dgrid, 256, 0, s>>>(o32, (const bf16_t*)d_o, (float*)workspace, B, T, H);
       dl = (const float*)workspace;
     }
-    int64_t grid = std::min<int64_t>(items, vit_cu_count());
+    // persistent: one workgroup per CU; VIT_FLAG_SHARED_CUS: one per item (no cross-item prefetch, any free CU)
+    int64_t grid = (flags & VIT_FLAG_SHARED_CUS) ? items : std::min<int64_t>(items, vit_cu_count());
     if (const char* e = getenv("VIT_ATTN_BWD_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(items, atoll(e)));
 #define BWD(NQ)                                                                                                  \
   attn_bwd_fused<NQ><<<(unsigned)grid, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \

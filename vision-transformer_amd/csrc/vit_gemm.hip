@@ -1777,7 +1777,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     {
       const char* pv = getenv("VIT_GEMM_PERSIST");
       const bool persist = launched != EPI_SLAB && launched != EPI_GENERAL && e.act != VIT_ACT_GELU &&
-                           !(pv && pv[0] == '0');
+                           !(d->flags & VIT_FLAG_SHARED_CUS) && !(pv && pv[0] == '0');
       if (persist && g4.nitems > vit_cu_count()) grid4.x = (unsigned)vit_cu_count();
     }
     e.csum = cs_fused ? d->colsum_part : nullptr;
