@@ -41,6 +41,12 @@ def main():
     print(f"attn fwd          {t:8.1f} us  {fl_f / t / 1e6:7.1f} TF (4 T^2 hd per head)")
     t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0), args.reps)
     print(f"attn bwd fused    {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF (10 T^2 hd per head)")
+    # the training configuration: the forward also stores O in fp32, the backward forms delta from it (attn_delta)
+    o32 = torch.empty(B * T, D, device="cuda")
+    t = timeit(lambda: _ops.attn_fwd(qkv, B, T, H, hd, 8.0, o32=o32), args.reps)
+    print(f"attn fwd +o32     {t:8.1f} us  {fl_f / t / 1e6:7.1f} TF")
+    t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, o32=o32), args.reps)
+    print(f"attn bwd +delta   {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF (attn_delta from o32 + fused)")
     os.environ["VIT_ATTN_BWD_SPLIT"] = "1"
     t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0), args.reps)
     print(f"attn bwd split    {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF")

@@ -7,6 +7,9 @@
 namespace {
 
 constexpr int LN_BWD_PARTS_MAX = 2048;
+#ifndef LN_BWD_RPB
+#define LN_BWD_RPB 32       // rows per backward block (its dgamma / dbeta partial covers them); 16 and 64 measured slower
+#endif
 
 template <class T, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int64_t ldx,
@@ -91,8 +94,11 @@ template <> struct Raw4<float> {
 // the value of v as stored in T (bf16 rounds to nearest even)
 template <class T> VIT_DEV float as_stored(float v) { return sizeof(T) == 2 ? bf2f(f2bf(v)) : v; }
 
-template <class T, int NV>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
+// AL (accumulators in LDS): the per-column dgamma / dbeta / output sums of each wave live in its own LDS region instead
+// of 3 x 4 x NV registers per lane, which takes the kernel from 3 to 4 waves per SIMD without spills (one more row of
+// loads in flight per SIMD); each lane only ever touches its own columns, so the row loop needs no barrier.
+template <class T, int NV, bool AL>
+__global__ __launch_bounds__(256, AL ? 4 : 1) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
                                                      int64_t ldx, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const T* __restrict__ dres, T* __restrict__ dx_out,
@@ -100,8 +106,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
                                                      uint32_t drop_seed, const uint8_t* __restrict__ drop_mask,
                                                      float* __restrict__ partial, int osum,
                                                      int64_t parts, int64_t rows, int64_t cols) {
-  __shared__ float red[3][256 * NV];
+  __shared__ __attribute__((aligned(16))) float red[AL ? 4 : 1][3][256 * NV];
+  __shared__ __attribute__((aligned(16))) float gms[AL ? 256 * NV : 4];     // AL: gamma, read per row from LDS
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (AL) {
+    for (int c = threadIdx.x * 4; c < 256 * NV; c += 1024) {
+      float g4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (c < cols) ld4<float>(gamma + c, g4);
+      *reinterpret_cast<f32x4*>(&gms[c]) = f32x4{g4[0], g4[1], g4[2], g4[3]};
+    }
+    __syncthreads();
+  }
   // whole groups of 4 rows per block and per wave step: a wave's 4 consecutive rows share one dword of a mask4
   const int64_t rows_per_part = (((rows + parts - 1) / parts) + 3) & ~(int64_t)3;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_part, r1 = min(rows, r0 + rows_per_part);
@@ -114,7 +129,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
     const int64_t c = ((int64_t)k * 64 + lane) * 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dg[k][r] = db[k][r] = os[k][r] = 0.f;
-    if (c < cols) ld4<float>(gamma + c, gm[k]);
+    if (AL)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) *reinterpret_cast<f32x4*>(&red[AL ? w : 0][s2][(k * 64 + lane) * 4]) = f32x4{};
+    if (AL) gm[k][0] = gm[k][1] = gm[k][2] = gm[k][3] = 0.f;      // unused: gms
+    else if (c < cols) ld4<float>(gamma + c, gm[k]);
     else gm[k][0] = gm[k][1] = gm[k][2] = gm[k][3] = 0.f;
   }
   // Wave w walks rows r0 + 4w + 16q + (0..3), q = 0, 1, ...: the next row's x / dy / residual (raw, packed) and mask
@@ -163,16 +182,40 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
     float sa = 0.f, sb = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
+      if (AL) {
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(&gms[(k * 64 + lane) * 4]);
+        gm[k][0] = g4[0];
+        gm[k][1] = g4[1];
+        gm[k][2] = g4[2];
+        gm[k][3] = g4[3];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {          // columns past `cols` have dv = gm = 0: they add exact zeros
         const float xh = (xv[k][r] - mu) * rs;
         const float g = dv[k][r] * gm[k][r];
         sa += g;
         sb += g * xh;
-        dg[k][r] += dv[k][r] * xh;
-        db[k][r] += dv[k][r];
+        if (!AL) {
+          dg[k][r] += dv[k][r] * xh;
+          db[k][r] += dv[k][r];
+        }
         xv[k][r] = xh;
         dv[k][r] = g;
+      }
+      if (AL) {
+        // the raw values are still in dc (dy) / xv (xhat): dg += dy * xhat, db += dy
+        float dyv[4];
+        Raw4<T>::unpack(dc[k], dyv);
+        f32x4* pg = reinterpret_cast<f32x4*>(&red[AL ? w : 0][0][(k * 64 + lane) * 4]);
+        f32x4* pb = reinterpret_cast<f32x4*>(&red[AL ? w : 0][1][(k * 64 + lane) * 4]);
+        f32x4 ag = *pg, ab = *pb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ag[r] += dyv[r] * xv[k][r];
+          ab[r] += dyv[r];
+        }
+        *pg = ag;
+        *pb = ab;
       }
     }
     const float a = wave_sum(sa) / (float)cols;
@@ -200,15 +243,42 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
           }
           st4<T>(drop_out + row * cols + c, dd);
           if (osum) {
+            if (AL) {
+              f32x4* po = reinterpret_cast<f32x4*>(&red[AL ? w : 0][2][(k * 64 + lane) * 4]);
+              f32x4 ao = *po;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) os[k][r] += dd[r];
+              for (int r = 0; r < 4; ++r) ao[r] += dd[r];
+              *po = ao;
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) os[k][r] += dd[r];
+            }
           }
         } else if (osum) {
+          if (AL) {
+            f32x4* po = reinterpret_cast<f32x4*>(&red[AL ? w : 0][2][(k * 64 + lane) * 4]);
+            f32x4 ao = *po;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) os[k][r] += as_stored<T>(o[r]);
+            for (int r = 0; r < 4; ++r) ao[r] += as_stored<T>(o[r]);
+            *po = ao;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) os[k][r] += as_stored<T>(o[r]);
+          }
         }
       }
     }
+  }
+  const int nset = osum ? 3 : 2;
+  const float oscale = drop_out ? drop_scale : 1.f;   // set 2 = column sums of drop_out * 1/(1-p)
+  if (AL) {                                           // the 4 wave regions, added in a fixed order
+    __syncthreads();
+    for (int64_t c = threadIdx.x; c < cols; c += 256)
+      for (int s2 = 0; s2 < nset; ++s2) {
+        const float v = ((red[0][s2][c] + red[AL ? 1 : 0][s2][c]) + red[AL ? 2 : 0][s2][c]) + red[AL ? 3 : 0][s2][c];
+        partial[(s2 * parts + blockIdx.x) * cols + c] = s2 == 2 ? v * oscale : v;
+      }
+    return;
   }
   // per-block partial sums: waves add into LDS in a fixed order (0, 1, 2, 3) -> bitwise reproducible
   for (int turn = 0; turn < 4; ++turn) {
@@ -219,23 +289,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
         for (int r = 0; r < 4; ++r) {
           const int cc = (k * 64 + lane) * 4 + r;
           if (turn == 0) {
-            red[0][cc] = dg[k][r];
-            red[1][cc] = db[k][r];
-            red[2][cc] = os[k][r];
+            red[0][0][cc] = dg[k][r];
+            red[0][1][cc] = db[k][r];
+            red[0][2][cc] = os[k][r];
           } else {
-            red[0][cc] += dg[k][r];
-            red[1][cc] += db[k][r];
-            red[2][cc] += os[k][r];
+            red[0][0][cc] += dg[k][r];
+            red[0][1][cc] += db[k][r];
+            red[0][2][cc] += os[k][r];
           }
         }
       }
     }
     __syncthreads();
   }
-  const int nset = osum ? 3 : 2;
-  const float oscale = drop_out ? drop_scale : 1.f;   // set 2 = column sums of drop_out * 1/(1-p)
   for (int64_t c = threadIdx.x; c < cols; c += 256)
-    for (int s = 0; s < nset; ++s) partial[(s * parts + blockIdx.x) * cols + c] = s == 2 ? red[s][c] * oscale : red[s][c];
+    for (int s = 0; s < nset; ++s) partial[(s * parts + blockIdx.x) * cols + c] = s == 2 ? red[0][s][c] * oscale : red[0][s][c];
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -372,7 +440,7 @@ int ln_fwd_launch(const T* x, int64_t ldx, const float* g, const float* b, T* y,
 
 extern "C" int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols) {
   (void)cols;
-  int64_t p = (rows + 15) / 16;  // >= 16 rows (4 per wave) per block; up to 2048 blocks (8 waves/SIMD in flight)
+  int64_t p = (rows + LN_BWD_RPB - 1) / LN_BWD_RPB;  // up to 2048 blocks
   if (p > LN_BWD_PARTS_MAX) p = LN_BWD_PARTS_MAX;
   if (p < 1) p = 1;
   return p;
@@ -424,16 +492,24 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
   const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   const float scale = 1.0f / (1.0f - drop_p);
   hipStream_t s = VIT_STREAM(stream);
+  // bf16 rows up to 1024 columns: per-wave accumulators in LDS (12 KiB x NV per block); VIT_LN_AL=0: registers
+  const char* al_env = getenv("VIT_LN_AL");
+  const bool al = !(al_env && al_env[0] == '0') && cols <= 1024;
   if (dtype == VIT_BF16) {
-#define CALLB(NV)                                                                                               \
-  ln_bwd_kernel<bf16_t, NV><<<(unsigned)parts, 256, 0, s>>>(                                                    \
-      (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
-      (bf16_t*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
+#define CALLB(NV)                                                                                                 \
+  if (al && NV <= 4)                                                                                              \
+    ln_bwd_kernel<bf16_t, NV, (NV <= 4)><<<(unsigned)parts, 256, 0, s>>>(                                         \
+        (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
+        (bf16_t*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols); \
+  else                                                                                                            \
+    ln_bwd_kernel<bf16_t, NV, false><<<(unsigned)parts, 256, 0, s>>>(                                             \
+        (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
+        (bf16_t*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLB)
 #undef CALLB
   } else {
 #define CALLF(NV)                                                                                            \
-  ln_bwd_kernel<float, NV><<<(unsigned)parts, 256, 0, s>>>(                                                  \
+  ln_bwd_kernel<float, NV, false><<<(unsigned)parts, 256, 0, s>>>(                                           \
       (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out,   \
       (float*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLF)
