@@ -148,20 +148,27 @@ def test_gemm_epilogue_bias_relu_dropout_residual(dtype):
     assert (out3.float() - ref3).abs().max().item() <= tol * max(1.0, ref3.abs().max().item())
 
 
-def test_gemm_row_group_and_rowmod():
-    """patch-embed epilogue: rows (b, n) -> b*T + n, + pos[n] (res_rowmod = N)"""
+@pytest.mark.parametrize("B,D", [(3, 256), (5, 768)])
+def test_gemm_row_group_and_rowmod(monkeypatch, B, D):
+    """patch-embed epilogue: rows (b, n) -> b*T + n, + pos[n] (res_rowmod = N); the dedicated wide kind (EPI_PATCH)
+    equals the general epilogue bit for bit and leaves the CLS rows alone"""
     torch.manual_seed(1)
-    B, N, T, D, K = 3, 196, 197, 256, 768
+    N, T, K = 196, 197, 768
     cols = torch.randn(B * N, K, device=DEV).bfloat16()
     w = (torch.randn(D, K, device=DEV) * 0.05).bfloat16()
     bias = torch.randn(D, device=DEV)
     pos = torch.randn(T, D, device=DEV)
-    x0 = torch.full((B * T, D), 7.0, device=DEV).bfloat16()
-    _ops.gemm(cols, w, x0, B * N, D, K, K, K, D, bias=bias, res=pos, ldres=D, res_rowmod=N, out_group=(N, T))
+    outs = []
+    for general in ("0", "1"):
+        monkeypatch.setenv("VIT_GEMM_EPI_GENERAL", general)
+        x0 = torch.full((B * T, D), 7.0, device=DEV).bfloat16()
+        _ops.gemm(cols, w, x0, B * N, D, K, K, K, D, bias=bias, res=pos, ldres=D, res_rowmod=N, out_group=(N, T))
+        outs.append(x0)
     ref = (cols.float() @ w.float().t() + bias).view(B, N, D) + pos[:N]
-    got = x0.view(B, T, D)
+    got = outs[0].view(B, T, D)
     assert (got[:, :N].float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
     assert torch.all(got[:, N] == 7.0)
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -524,7 +524,9 @@ enum EpiKind : int {
   EPI_BDR = 3,        // dropout(alpha * acc [+ bias]) [+ res]
   EPI_SLAB = 4,       // split-K fp32 slab
   EPI_GENERAL = 5,    // epilogue4 (beta, row groups, row-modulo residual, unaligned, any combination)
-  EPI_AUXM = 6        // alpha * acc masked by a mask4 bit (ReLU backward from the forward's stored mask)
+  EPI_AUXM = 6,       // alpha * acc masked by a mask4 bit (ReLU backward from the forward's stored mask)
+  EPI_PATCH = 7       // alpha * acc + bias + res_f32[i % res_rowmod] stored at row (i / G) * Gs + i % G: the
+                      // patch embedding (conv bias, + pos, patch rows -> token rows; vit.py:21-29,42)
 };
 
 // Kinds whose row epilogue reads a second [m][n]-shaped bf16 operand (ReLU mask / residual).  Those reads are
@@ -902,9 +904,18 @@ VIT_DEV uint32_t v4_epi_row8(const EpiParams& e, int64_t i, int64_t j, bf16_t* c
                              float (&v)[8], uint4 pre, int sh) {
 #pragma unroll
   for (int r = 0; r < 8; ++r) v[r] *= e.alpha;
-  if (KIND == EPI_BIAS_ACT || KIND == EPI_BDR) {
+  if (KIND == EPI_BIAS_ACT || KIND == EPI_BDR || KIND == EPI_PATCH) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] += b8[r];
+  }
+  if (KIND == EPI_PATCH) {                  // + the fp32 residual row i % rowmod (pos, 605 KB: L2-resident)
+    const float* rp = (const float*)e.res + (int64_t)((int)i % (int)e.res_rowmod) * e.ldres + j;
+    const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] += r0[r];
+      v[r + 4] += r1[r];
+    }
   }
   if (KIND == EPI_BIAS_ACT && ACT == 1) {
 #pragma unroll
@@ -1116,7 +1127,7 @@ VIT_DEV void v4_epilogue_d(const EpiParams& e, f32x4 (&acc)[2][2][4][2], float* 
   for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
     for (int r = 0; r < 8; ++r) b8[nh][r] = 0.f;
-  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR) && e.bias) {
+  if ((KIND == EPI_BIAS_ACT || KIND == EPI_BDR || KIND == EPI_PATCH) && e.bias) {
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh) {
       const int64_t j = j0 + nh * 128 + wc * 32 + cq;
@@ -1155,7 +1166,9 @@ VIT_DEV void v4_epilogue_d(const EpiParams& e, f32x4 (&acc)[2][2][4][2], float* 
         if (v[0] != 1234.5f) continue;
 #endif
         if (i < e.m && j < e.n) {
-          bits = v4_epi_row8<KIND, ACT, MK, CS>(e, i, j, (bf16_t*)e.c + i * e.ldc + j, b8[nh], v,
+          // EPI_PATCH: output row (i / G) * Gs + i % G (32-bit: the host bounds m)
+          const int64_t orow = KIND == EPI_PATCH ? (int64_t)((int)i / (int)e.grp) * e.grp_stride + (int)i % (int)e.grp : i;
+          bits = v4_epi_row8<KIND, ACT, MK, CS>(e, i, j, (bf16_t*)e.c + orow * e.ldc + j, b8[nh], v,
                                                 has_pre ? pre[nh][x] : make_uint4(0u, 0u, 0u, 0u), 8 * (int)(i & 3));
           if (CS) {
 #pragma unroll
@@ -1761,6 +1774,10 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
       kind = EPI_AUXM;
     else if (fast && !e.aux && e.act == VIT_ACT_NONE && (e.use_drop || e.res) && (!e.res || e.res_dtype == VIT_BF16))
       kind = EPI_BDR;
+    else if (e.vec && e.beta == 0.f && e.grp > 0 && e.res_rowmod > 0 && e.bias && e.res && e.res_dtype == VIT_F32 &&
+             e.act == VIT_ACT_NONE && !e.aux && !e.use_drop && d->m < 0x7fffffffLL && d->ldres % 8 == 0 &&
+             aligned(d->res, 16))
+      kind = EPI_PATCH;
     const char* dk = getenv("VIT_GEMM_EPI_GENERAL");      // A/B switch: force the general epilogue
     if (dk && dk[0] == '1' && kind != EPI_SLAB) kind = EPI_GENERAL;
     // the v4 epilogue instantiation that runs (fast kinds exist for bf16 output and these operand layouts only)
@@ -1770,6 +1787,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     else if (out_bf && akc && bkc && (kind == EPI_BIAS_ACT || kind == EPI_BDR)) launched = kind;
     else if (out_bf && akc && !bkc && kind == EPI_AUX) launched = EPI_AUX;
     else if (out_bf && akc && !bkc && kind == EPI_AUXM) launched = EPI_AUXM;
+    else if (out_bf && akc && bkc && kind == EPI_PATCH) launched = EPI_PATCH;
     if (launched != EPI_SLAB && launched != EPI_GENERAL && !e.vec8) launched = EPI_GENERAL;  // wide epilogue needs 8-wide rows
     cs_fused = v4 && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
     // persistent grid (one workgroup per CU looping over items) for the wide-epilogue kinds; VIT_GEMM_PERSIST=0: one
@@ -1792,6 +1810,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
       else if (AK && BKK && launched == EPI_BDR) V4(AK, BKK, bf16_t, EPI_BDR);                                 \
       else if (AK && !BKK && launched == EPI_AUX) V4(AK, BKK, bf16_t, EPI_AUX);                                \
       else if (AK && !BKK && launched == EPI_AUXM) V4(AK, BKK, bf16_t, EPI_AUXM);                              \
+      else if (AK && BKK && launched == EPI_PATCH) V4(AK, BKK, bf16_t, EPI_PATCH);                             \
       else V4(AK, BKK, bf16_t, EPI_GENERAL);                                                                   \
     } else if (v2) {                                                                                           \
       if (out_bf && split == 1) gemm_bf16_v2<AK, BKK, bf16_t><<<grid, block, 0, s>>>(g, e, a_bytes, b_bytes);     \
