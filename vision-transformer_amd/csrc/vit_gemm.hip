@@ -1659,7 +1659,11 @@ extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dty
   if (m <= 0 || n <= 0 || k <= 0) return 1;
   if (in_dtype == VIT_BF16 && k % BK == 0 && gemm_impl(m, n) == 4) {
     const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
-    const int64_t s = std::min<int64_t>(std::min<int64_t>(256 / tiles, (k / BK) / 4), 64);
+    // slices of >= 4 k-tiles; reductions of fewer than 16 k-tiles (the pruned last block's weight gradients: K = B)
+    // may go down to 1 k-tile per slice (VIT_SPLITK_MINKT overrides the minimum)
+    static const int64_t min_env = [] { const char* e = getenv("VIT_SPLITK_MINKT"); return e ? atoll(e) : 0; }();
+    const int64_t nkt = k / BK, min_kt = min_env > 0 ? min_env : (nkt >= 16 ? 4 : 1);
+    const int64_t s = std::min<int64_t>(std::min<int64_t>(256 / tiles, nkt / min_kt), 64);
     return (int)std::max<int64_t>(1, s);
   }
   // 128x128 tiles, two per CU, two rounds (also the fp32 parity path's split: its summation order is part of the
