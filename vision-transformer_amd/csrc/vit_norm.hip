@@ -441,6 +441,8 @@ int ln_fwd_launch(const T* x, int64_t ldx, const float* g, const float* b, T* y,
 extern "C" int64_t vit_layernorm_bwd_parts(int64_t rows, int64_t cols) {
   (void)cols;
   int64_t p = (rows + LN_BWD_RPB - 1) / LN_BWD_RPB;  // up to 2048 blocks
+  // few rows (the classifier head's LN: B rows x 4D): spread them, >= 4 rows per block, up to 256 blocks
+  if (p < 256) p = std::max<int64_t>(p, std::min<int64_t>(256, (rows + 3) / 4));
   if (p > LN_BWD_PARTS_MAX) p = LN_BWD_PARTS_MAX;
   if (p < 1) p = 1;
   return p;
