@@ -12,7 +12,7 @@ With `--gpus N > 1` and no torchrun environment, bench.py starts the N ranks its
 makes no GPU call).  `--dry-run` replaces the HIP model by a CPU stand-in on gloo, to test the launch plumbing without
 a GPU.  Rank 0 prints ONE JSON line.
 
-Live roofline: HIP events on the compute stream bracket every hot launch of the step, grouped into families
+Live roofline: HIP events on the compute stream bracket every hot launch of the last timed step, grouped into families
 (forward / dgrad / wgrad GEMMs, attention fwd/bwd, LayerNorm fwd/bwd), each launch carrying its algorithmic FLOPs and
 HBM bytes.  `roofline` reports the family that takes the most time; `roofline_families`
 reports all of them.  `traffic` is the measured HBM bytes per launch of that family (rocprofv3 PMC passes under
@@ -246,12 +246,14 @@ def run(args, rank, world, local):
     if world > 1:
         dist.barrier()
     sync()
-    timer = None
-    if not args.dry_run and not args.no_roofline:
-        timer = FamilyTimer()
-        model.hip_engine.profile_hook = timer
+    # The live roofline brackets every hot launch of the LAST timed step with HIP events (each event record is a
+    # stream barrier: on every step they cost ~1.4 ms of the ~36 ms step, measured; on one step of K they cost ~1.4/K)
+    timer = FamilyTimer() if not args.dry_run and not args.no_roofline else None
+    roof_steps = 1 if timer is not None else 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if timer is not None and i == args.steps - roof_steps:
+            model.hip_engine.profile_hook = timer
         loss = step()
     sync()
     if world > 1:
@@ -299,7 +301,7 @@ def run(args, rank, world, local):
             out["gflop_per_image"] = round(gf, 3)
             out["final_loss"] = round(final_loss, 4)
             if timer is not None:
-                fams = timer.summary(args.steps)
+                fams = timer.summary(roof_steps)
                 dom = max(fams, key=lambda f: fams[f]["ms_per_step"])
                 d = fams[dom]
                 key = workload_key(args)
@@ -320,6 +322,7 @@ def run(args, rank, world, local):
                     "pmc_mfma_busy_frac": pmc.get("mfma_busy_frac") if pmc else None,
                     "traffic_source": f"profiles/pmc_{key}.json" if traffic is not None else None,
                     "ms_per_step": d["ms_per_step"], "launches_per_step": d["launches_per_step"],
+                    "events_over": "every hot launch of the last of the timed steps (HIP events on the compute stream)",
                     "avg_launch_us": d["avg_launch_us"],
                     "kernels": {"gemm_wgrad": "gemm_bf16_v4<false,false,float,EPI_SLAB> + splitk_reduce",
                                 "gemm_fwd": "gemm_bf16_v4<true,true,bf16,*>", "gemm_dgrad": "gemm_bf16_v4<true,false,*>",
