@@ -98,7 +98,7 @@ template <class T> VIT_DEV float as_stored(float v) { return sizeof(T) == 2 ? bf
 // of 3 x 4 x NV registers per lane, which takes the kernel from 3 to 4 waves per SIMD without spills (one more row of
 // loads in flight per SIMD); each lane only ever touches its own columns, so the row loop needs no barrier.
 template <class T, int NV, bool AL>
-__global__ __launch_bounds__(256, AL ? 4 : 1) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
+__global__ __launch_bounds__(256, AL && NV <= 4 ? 4 : 1) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
                                                      int64_t ldx, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      const T* __restrict__ dres, T* __restrict__ dx_out,
@@ -510,10 +510,17 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
     NV_SWITCH(cols, CALLB)
 #undef CALLB
   } else {
+  // fp32 (the parity path and the classifier head's LN(4D)): LDS accumulators for the wide rows (NV 6-12), whose
+  // register form spilled ~350 VGPRs (the head's LN backward, B x 3072: 133 -> 26.5 us)
 #define CALLF(NV)                                                                                            \
-  ln_bwd_kernel<float, NV, false><<<(unsigned)parts, 256, 0, s>>>(                                           \
-      (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out,   \
-      (float*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
+  if (NV >= 6 && NV <= 12 && !(al_env && al_env[0] == '0'))                                                  \
+    ln_bwd_kernel<float, NV, (NV >= 6 && NV <= 12)><<<(unsigned)parts, 256, 0, s>>>(                         \
+        (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out, \
+        (float*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols); \
+  else                                                                                                       \
+    ln_bwd_kernel<float, NV, false><<<(unsigned)parts, 256, 0, s>>>(                                         \
+        (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out, \
+        (float*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols)
     NV_SWITCH(cols, CALLF)
 #undef CALLF
   }
