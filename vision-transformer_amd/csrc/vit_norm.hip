@@ -494,13 +494,13 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
   const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   const float scale = 1.0f / (1.0f - drop_p);
   hipStream_t s = VIT_STREAM(stream);
-  // bf16 rows up to 1024 columns: per-wave accumulators in LDS (12 KiB x NV per block); VIT_LN_AL=0: registers
+  // bf16 rows up to 3072 columns: per-wave accumulators in LDS (13 KiB x NV per block); VIT_LN_AL=0: registers
   const char* al_env = getenv("VIT_LN_AL");
-  const bool al = !(al_env && al_env[0] == '0') && cols <= 1024;
+  const bool al = !(al_env && al_env[0] == '0');
   if (dtype == VIT_BF16) {
 #define CALLB(NV)                                                                                                 \
-  if (al && NV <= 4)                                                                                              \
-    ln_bwd_kernel<bf16_t, NV, (NV <= 4)><<<(unsigned)parts, 256, 0, s>>>(                                         \
+  if (al && NV <= 12)                                                                                             \
+    ln_bwd_kernel<bf16_t, NV, (NV <= 12)><<<(unsigned)parts, 256, 0, s>>>(                                         \
         (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, gamma, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx_out,  \
         (bf16_t*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols); \
   else                                                                                                            \
