@@ -674,11 +674,27 @@ VIT_DEV void dma_offsets4g(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int
   }
 }
 
+// The two pieces are issued as inline asm, not __builtin_amdgcn_global_load_lds: the compiler's waitcnt pass cannot
+// tell an LDS-DMA target from the ds_read_b64_tr_b16 reads of the other ring slots and put `s_waitcnt vmcnt(0)` in
+// front of the transposed-operand reads of every phase (2 per k-tile on the dgrad layout, 3 on the weight-gradient
+// layout), draining the stages the ring keeps in flight.  Completion is ordered explicitly everywhere the slots are
+// read (wait_stage_retired + barrier in the k-loop, vmcnt(0) before the epilogue image and the next item).
 VIT_DEV void dma_half_g(const char* base, const uint32_t (&off)[2], uint32_t soff, bf16_t* half, int wave) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(base + off[i] + soff),
-                                     (__attribute__((address_space(3))) void*)(half + (wave * 2 + i) * 512), 16, 0, 0);
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(half + wave * 2 * 512));
+  const char* p0 = base + off[0] + soff;
+  const char* p1 = base + off[1] + soff;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile(
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off\n\t"
+      "s_add_u32 m0, %2, 0x400\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off" ::"v"(p0), "v"(p1), "s"(lds)
+      : "memory", "m0");
+#pragma clang diagnostic pop
 }
 
 VIT_DEV void dma_half(__amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[2], uint32_t soff, bf16_t* half, int wave) {
