@@ -38,7 +38,12 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16 = 2.5e15      # dense bf16 MFMA, MI355X (MI355X_MICROARCH.md chip table; no sparsity)
 PEAK_F32 = 157.3e12     # fp32 MFMA
 PEAK_HBM = 8.0e12       # HBM3E bytes/s
-METRIC = "images/sec fwd+bwd ViT-Base/16 224^2 bf16 (train step incl. AdamW); % MFMA roofline"
+
+
+def metric_name(args):
+    """The headline metric string for this workload (BASELINE.json metric for ViT-Base/16 224^2 bf16)."""
+    return (f"images/sec fwd+bwd ViT-{args.model.capitalize()}/16 {args.img}^2 {args.dtype} (train step incl. AdamW); "
+            f"% MFMA roofline")
 
 
 def gflop_per_image(D, L, T, N, P, C, nc):
@@ -47,6 +52,14 @@ def gflop_per_image(D, L, T, N, P, C, nc):
     block = 24.0 * T * D * D + 4.0 * T * T * D
     head = 2.0 * D * 4 * D + 2.0 * 4 * D * nc
     return (2 * pe + 3 * (L * block + head)) / 1e9
+
+
+def gflop_executed_per_image(D, L, T, N, P, C, nc, pruned):
+    """GFLOP per image the kernels actually execute: the reference count minus the last block's proj / fc1 / fc2
+    (fwd, dgrad, wgrad: 54 D^2 per token) on the T-1 rows the pruned last block skips (its outputs and
+    gradients are identical to the unpruned engine's, tested)."""
+    full = gflop_per_image(D, L, T, N, P, C, nc)
+    return full - (54.0 * D * D * (T - 1) / 1e9 if pruned else 0.0)
 
 
 def workload_key(args):
@@ -97,11 +110,10 @@ def log(msg):
 
 
 def host_topology():
-    """Threads this process may use — the CPUs in its affinity mask, capped by the machine's OMP_NUM_THREADS share
-    when one is set (the GPU box exports 16 per GPU) — plus sockets / physical cores of the host (/proc/cpuinfo)."""
+    """CPUs this process may use (its affinity mask), the machine's OMP_NUM_THREADS share when one is set (the GPU
+    box exports 16 per GPU), plus sockets / physical cores of the host (/proc/cpuinfo)."""
     affinity = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(affinity, share) if share > 0 else affinity
     sockets, cores = set(), set()
     try:
         phys = core = None
@@ -117,22 +129,20 @@ def host_topology():
                     phys = core = None
     except OSError:
         pass
-    return {"threads_used": threads, "affinity_cpus": affinity, "omp_num_threads": share or None,
-            "host_logical_cpus": os.cpu_count(), "sockets": len(sockets) or None, "physical_cores": len(cores) or None}
+    return {"affinity_cpus": affinity, "omp_num_threads": share or None, "host_logical_cpus": os.cpu_count(),
+            "sockets": len(sockets) or None, "physical_cores": len(cores) or None}
 
 
-def cpu_baseline(img, nc, budget_s=20.0):
-    """The repo's own CPU training step (train.py time_steps -> VisionTransformer/_cpu.py, torch.optim.AdamW) on every
-    core this process may use.  C1 exactly (ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 timed steps), then ViT-Base/16
-    img^2 fp32 B32: 1 warmup step, then as many timed steps (1-3) as fit in ~budget_s."""
+def _cpu_leg(img, nc, threads, budget_s):
+    """C1 exactly (ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 timed steps), then ViT-Base/16 img^2 fp32 B32: 1 warmup
+    step, then as many timed steps (1-3) as fit in ~budget_s, on `threads` threads."""
     import train as T
     from VisionTransformer import config
-    topo = host_topology()
     prev = torch.get_num_threads()
-    torch.set_num_threads(topo["threads_used"])
+    torch.set_num_threads(threads)
     try:
         c1 = config.ViTConfig(3, 10, 16, 192, 16, 3, 12, "cpu", 8)
-        log(f"cpu baseline: C1 on {topo['threads_used']} threads")
+        log(f"cpu baseline: C1 on {threads} threads")
         s1, _ = T.time_steps(c1, steps=30, warmup=5, dev="cpu")
         log(f"cpu baseline: C1 {s1 * 1e3:.1f} ms/step; ViT-B B32 warmup step")
         cb = config.ViTConfig.preset("base", img_size=img, batch_size=32, num_classes=nc, precision=torch.float32,
@@ -145,13 +155,28 @@ def cpu_baseline(img, nc, budget_s=20.0):
         sb, _ = T.time_steps(cb, steps=steps, warmup=1, dev="cpu")
     finally:
         torch.set_num_threads(prev)
-    return {"value": round(32 / sb, 3), "unit": "images/s", "cores": topo["threads_used"], "kind": "port",
-            "sample": f"repo train.py host step (VisionTransformer/_cpu.py fwd+CE+bwd + torch AdamW, dropout on), "
-                      f"ViT-Base/16 {img}^2 fp32 B32, 1 warmup + {steps} timed steps, "
-                      f"{topo['threads_used']} threads",
-            "topology": topo,
+    return {"images_per_s": round(32 / sb, 3), "steps": steps, "threads": threads,
             "c1": {"workload": "BASELINE config 1: ViT-Tiny/16 64^2 B8 fp32, 5 warmup + 30 timed steps",
                    "ms_per_step": round(s1 * 1e3, 3), "images_per_s": round(8 / s1, 3)}}
+
+
+def cpu_baseline(img, nc, budget_s=20.0):
+    """The repo's own CPU training step (train.py time_steps -> VisionTransformer/_cpu.py, torch.optim.AdamW) on every
+    CPU in this process's affinity mask (the value), and again on the box's OMP_NUM_THREADS share when that is
+    smaller (`share`)."""
+    topo = host_topology()
+    full = _cpu_leg(img, nc, topo["affinity_cpus"], budget_s)
+    out = {"value": full["images_per_s"], "unit": "images/s", "cores": full["threads"], "kind": "port",
+           "sample": f"repo train.py host step (VisionTransformer/_cpu.py fwd+CE+bwd + torch AdamW, dropout on), "
+                     f"ViT-Base/16 {img}^2 fp32 B32, 1 warmup + {full['steps']} timed steps, "
+                     f"{full['threads']} threads (every CPU of the affinity mask)",
+           "topology": topo, "c1": full["c1"]}
+    share = topo["omp_num_threads"]
+    if share and share < topo["affinity_cpus"]:
+        sh = _cpu_leg(img, nc, share, budget_s)
+        out["share"] = {"threads": share, "images_per_s": sh["images_per_s"], "c1": sh["c1"],
+                        "note": "the GPU box's OMP_NUM_THREADS share per GPU"}
+    return out
 
 
 class FamilyTimer:
@@ -203,11 +228,14 @@ def run(args, rank, world, local):
     if args.dry_run:          # launch-plumbing stand-in: one small CPU GEMM + a gradient-sized all-reduce per step
         w = torch.randn(256, 256)
         g = torch.zeros(1 << 16)
+        comm_ms = [None]
 
         def step():
             y = (w @ w).sum()
             if world > 1:
+                t = time.perf_counter()
                 dist.all_reduce(g)
+                comm_ms[0] = (time.perf_counter() - t) * 1e3      # the stand-in's all-reduce is fully exposed
             return y
         D = L = T = N = 0
         cfg = None
@@ -219,7 +247,7 @@ def run(args, rank, world, local):
         torch.manual_seed(0)                       # identical init on every rank (reference init order, CPU RNG)
         model = vit.VisionTransformer(cfg).to(dev).train()
         if world > 1:
-            model.enable_data_parallel()
+            model.enable_data_parallel(grad_dtype=torch.bfloat16 if args.grad_comm == "bf16" else torch.float32)
         opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
         gen = torch.Generator().manual_seed(1234 + rank)
         x = torch.randn(args.batch, 3, args.img, args.img, generator=gen).to(dev)
@@ -254,6 +282,8 @@ def run(args, rank, world, local):
     for i in range(args.steps):
         if timer is not None and i == args.steps - roof_steps:
             model.hip_engine.profile_hook = timer
+        if world > 1 and not args.dry_run and i == args.steps - 1:
+            model.hip_engine.time_comm = True         # events around the bucket waits of the last step
         loss = step()
     sync()
     if world > 1:
@@ -267,6 +297,16 @@ def run(args, rank, world, local):
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    comm = None
+    if world > 1:
+        # exposed all-reduce time of the last timed step (compute stream idle after its last backward kernel until
+        # the last bucket is averaged), max over ranks
+        c = comm_ms[0] if args.dry_run else model.hip_engine.comm_exposed_ms()
+        if not args.dry_run:
+            model.hip_engine.time_comm = False
+        ct = torch.tensor([c if c is not None else -1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(ct, op=dist.ReduceOp.MAX)
+        comm = float(ct.item()) if ct.item() >= 0 else None
     final_loss = float(loss.item())
     log(f"rank {rank}/{world}: {elapsed / args.steps * 1e3:.2f} ms/step")
 
@@ -274,7 +314,7 @@ def run(args, rank, world, local):
         ms = elapsed / args.steps * 1e3
         imgs = world * args.batch * args.steps / elapsed
         out = {
-            "metric": METRIC,
+            "metric": metric_name(args),
             "value": round(imgs, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -291,6 +331,9 @@ def run(args, rank, world, local):
                        "model": f"vit_{args.model}_patch16_{args.img}", "global_batch": args.batch * world,
                        "seq_len": T, "parallelism": f"dp{world}"},
         }
+        if world > 1:
+            out["comm_exposed_ms"] = round(comm, 3) if comm is not None else None
+            out["grad_comm_dtype"] = args.grad_comm
         if args.dry_run:
             out["dry_run"] = True
             out["data"] = "dry run: CPU stand-in step on gloo, no HIP model (launch plumbing only)"
@@ -299,6 +342,9 @@ def run(args, rank, world, local):
             peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
             out["step_mfma_frac"] = round(imgs * gf * 1e9 / (world * peak), 4)
             out["gflop_per_image"] = round(gf, 3)
+            gfx = gflop_executed_per_image(D, L, T, N, cfg.patch_size, 3, args.classes, model.hip_engine.prune_last)
+            out["step_mfma_frac_executed"] = round(imgs * gfx * 1e9 / (world * peak), 4)
+            out["gflop_executed_per_image"] = round(gfx, 3)
             out["final_loss"] = round(final_loss, 4)
             if timer is not None:
                 fams = timer.summary(roof_steps)
@@ -368,6 +414,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
+                    help="dtype of the gradient all-reduce buckets for N > 1 (bf16: half the xGMI bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events (profiling runs)")

@@ -11,7 +11,8 @@
  *   - `stream` is a hipStream_t passed as void*; every launch is asynchronous on it; no device sync, no allocation
  *     (callers own all buffers and workspaces — the PyTorch caching allocator in the host package);
  *   - return 0 on success, a nonzero vit_status on failure with a thread-local message in vit_last_error();
- *   - re-entrant; no global mutable state.
+ *   - re-entrant; the only process-wide state is the option table of vit_set_option (below), whose defaults are the
+ *     shipped configuration.  The library never reads the environment.
  */
 #ifndef VIT_HIP_H
 #define VIT_HIP_H
@@ -22,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 8
+#define VIT_ABI_VERSION 9
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -42,6 +43,26 @@ typedef enum { VIT_ACT_NONE = 0, VIT_ACT_RELU = 1, VIT_ACT_GELU = 2 } vit_act;
 
 int vit_abi_version(void);
 const char* vit_last_error(void);
+
+/* Launch options (process-wide; every name's default is the shipped configuration).  They choose between kernel
+ * variants that compute the same function — A/B runs and the per-variant tests use them — and are the only switches
+ * the library has: nothing is read from the environment, so a user's environment cannot change which kernels run.
+ *   "gemm_impl"          0 automatic (default); 1 / 2 / 4 force the bf16 GEMM kernel generation (register-staged
+ *                        128x128 / LDS-DMA 128x128 / LDS-DMA 256x256 ping-pong)
+ *   "gemm_tail"          1 (default): split-K tail for a last round of 256x256 tiles that fills at most half the CUs
+ *   "gemm_tail_min_kt"   32: minimum k-tiles (K / 64) for that tail
+ *   "splitk_min_kt"      0 (automatic): minimum k-tiles per K-slice in vit_gemm_split_k_hint
+ *   "gemm_group_m"       0 (automatic): tile-row group size of the 256x256 tile order
+ *   "gemm_epi_general"   0: 1 forces the general (unspecialised) GEMM epilogue
+ *   "gemm_persist"       1: persistent one-workgroup-per-CU grid for the wide-epilogue GEMM kinds (0: one per tile)
+ *   "attn_fwd_split"     0: 1 forces the tiled attention forward for T <= 256
+ *   "attn_bwd_split"     0: 1 forces the tiled attention backward for T <= 256
+ *   "attn_bwd_grid"      0 (automatic): workgroups of the persistent attention backward
+ *   "ln16"               1: the 16-B-per-lane LayerNorm forward where the layout allows it
+ *   "ln_al"              1: LayerNorm backward accumulators in LDS (0: registers)
+ * vit_set_option returns VIT_ERR_INVALID for an unknown name; vit_get_option returns INT64_MIN for one. */
+int vit_set_option(const char* name, int64_t value);
+int64_t vit_get_option(const char* name);
 
 /* ------------------------------------------------------------------------------------------------------------
  * GEMM with fused epilogue:  C[i][j] = epi( alpha * sum_r A(i,r) * B(j,r) )
@@ -94,7 +115,7 @@ typedef struct vit_gemm_desc {
 
 /* Workspace vit_gemm can use: split_k > 1: the K-split fp32 slabs (required).  split_k <= 1: the slabs of the split-K
  * tail (when the 256x256 tiles leave the last round of the 256 CUs at most half full, those tile rows run split-K
- * over the idle CUs; VIT_GEMM_TAIL=0 disables it), or 0.  Without it (NULL / too small) the GEMM runs unsplit. */
+ * over the idle CUs; option "gemm_tail" 0 disables it), or 0.  Without it (NULL / too small) the GEMM runs unsplit. */
 int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d);
 /* Recommended split_k for C[m][n] with reduction depth k and input dtype (VIT_BF16 / VIT_F32) on the kernel vit_gemm
  * will pick: fills one round of the 256 CUs with output tiles x K-slices, each slice >= 4 (bf16) / 8 (f32)

@@ -20,3 +20,18 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture
+def libopt():
+    """Set libvit_hip launch options (vit_set_option) for one test; every option is restored at teardown."""
+    from VisionTransformer import _lib
+    saved = {}
+
+    def set_(name, value):
+        prev = _lib.set_option(name, value)
+        saved.setdefault(name, prev)
+
+    yield set_
+    for name, value in saved.items():
+        _lib.set_option(name, value)

@@ -146,6 +146,8 @@ def test_bench_spawns_ranks_dry_run():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 512
     assert out["dry_run"] is True and out["value"] > 0
+    assert "comm_exposed_ms" in out and out["comm_exposed_ms"] is not None and out["comm_exposed_ms"] >= 0
+    assert out["grad_comm_dtype"] == "fp32"
 
 
 def test_library_exports_every_header_symbol():
@@ -157,6 +159,27 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert lib.vit_abi_version() == _lib.ABI_VERSION
+
+
+def test_library_options_host_only():
+    """vit_set_option / vit_get_option (vit_hip.h): the documented names and shipped defaults, set/restore, and an
+    unknown name refused — host-side only, and the library never reads the environment (no getenv in csrc/)."""
+    defaults = {"gemm_impl": 0, "gemm_tail": 1, "gemm_tail_min_kt": 32, "splitk_min_kt": 0, "gemm_group_m": 0,
+                "gemm_epi_general": 0, "gemm_persist": 1, "attn_fwd_split": 0, "attn_bwd_split": 0,
+                "attn_bwd_grid": 0, "ln16": 1, "ln_al": 1}
+    for k, v in defaults.items():
+        assert _lib.get_option(k) == v, k
+    with _lib.option("gemm_persist", 0):
+        assert _lib.get_option("gemm_persist") == 0
+    assert _lib.get_option("gemm_persist") == 1
+    with pytest.raises(RuntimeError):
+        _lib.set_option("no_such_option", 1)
+    with pytest.raises(KeyError):
+        _lib.get_option("no_such_option")
+    csrc = os.path.join(ROOT, "vision-transformer_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h")):
+            assert "getenv" not in open(os.path.join(csrc, f)).read(), f
 
 
 def test_dropout_seed_twins():
@@ -222,7 +245,7 @@ def _free_port():
     return port
 
 
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, port, q, comm_dtype=torch.float32):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -232,24 +255,58 @@ def _ddp_worker(rank, world, port, q):
     eng = m.hip_engine
     eng._build(m, torch.device("cpu"))
     eng.ddp_enabled = True
-    eng.G.copy_(torch.arange(eng.G.numel(), dtype=torch.float32) * (rank + 1))
+    eng.comm_dtype = comm_dtype
+    # rank-dependent values that are not bf16-exact, so the bf16 path's rounding is visible
+    base = torch.arange(eng.G.numel(), dtype=torch.float32) / 7.0 + 0.001
+    eng.G.copy_(base * (rank + 1))
     for rng in [eng.head_range] + [eng.block_range[l] for l in reversed(range(2))] + [eng.embed_range]:
         eng._bucket_ready(rng)
     eng._finish_buckets()
-    expect = torch.arange(eng.G.numel(), dtype=torch.float32) * (sum(range(1, world + 1)) / world)
-    q.put((rank, bool(torch.allclose(eng.G, expect))))
+    ranks = [base * (r + 1) for r in range(world)]
+    if comm_dtype == torch.bfloat16:
+        # each rank's gradients rounded to bf16, summed in bf16 (gloo), widened and averaged
+        acc = ranks[0].bfloat16()
+        for g in ranks[1:]:
+            acc = acc + g.bfloat16()
+        expect = acc.float() * (1.0 / world)
+        ok = torch.equal(eng.G, expect)
+    else:
+        ok = torch.allclose(eng.G, sum(ranks) / world)
+    q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
 
-def test_ddp_gradient_buckets_gloo():
+@pytest.mark.parametrize("comm_dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_ddp_gradient_buckets_gloo(comm_dtype):
+    """2-rank gloo: every bucket of the flat gradient buffer is averaged across ranks; with bf16 buckets
+    (enable_data_parallel(grad_dtype=torch.bfloat16)) the result is exactly the average of the bf16-rounded
+    gradients."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q, comm_dtype)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def test_attention_probs_warns_once_after_fused_forward():
+    """The fused forward keeps attention probabilities only with store_attention_probs=True; reading them after a
+    forward that skipped them returns None (as before) but warns once, pointing at the flag."""
+    import warnings
+    mh = transformer.MultiHeadAttention(2, 8, 16, 5)
+    assert mh.attention_probs is None                     # never ran: no warning
+    transformer._PROBS_WARNED = False
+    mh.attention_probs = None
+    mh._probs_skipped = True                              # what the engine records after a fused forward
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert mh.attention_probs is None
+        assert mh.attention_probs is None
+    assert len(w) == 1 and "store_attention_probs" in str(w[0].message)
+    mh.attention_probs = torch.zeros(1)                   # module-level forward stores them: no warning path
+    assert mh.attention_probs is not None and not mh._probs_skipped

@@ -293,6 +293,32 @@ def test_parameter_hooks_run_once_per_backward():
     assert torch.allclose(g_half, 0.5 * w2.grad)
 
 
+def test_parameter_hooks_with_gradient_accumulation():
+    """Two backwards without zero_grad: a `register_hook` hook transforms each backward's gradient only,
+    as autograd's does — 0.5 g1 + 0.5 g2, not 0.5 (0.5 g1 + g2) — and hook-free parameters accumulate exactly as
+    without hooks."""
+    ocfg = _hd64_cfg()
+    st = O.init_state(ocfg, seed=12)
+    x, y = O.synthetic_batch(ocfg)
+    x, y = x.to(DEV), y.to(DEV)
+
+    def run(hook):
+        m = _model(ocfg, st).eval()
+        if hook:
+            m.transformer_encoder.blocks[0].multi_head.heads[1].value.weight.register_hook(lambda g: g * 0.5)
+        for _ in range(2):
+            cross_entropy(m(x), y).backward()
+        return dict(m.named_parameters())
+
+    hooked, plain = run(True), run(False)
+    key = "transformer_encoder.blocks.0.multi_head.heads.1.value.weight"
+    # same input twice in eval mode: g1 == g2, so autograd gives g1 = 0.5 * (g1 + g2) exactly
+    assert torch.equal(hooked[key].grad, 0.5 * plain[key].grad)
+    for k, p in hooked.items():
+        if k != key:
+            assert torch.allclose(p.grad, plain[k].grad, rtol=1e-6, atol=1e-7), k
+
+
 def test_deepcopy_snapshot_is_independent():
     """A deep copy (EMA / best-model snapshot) builds its own engine: same outputs, and training the original does
     not touch the copy."""
@@ -392,3 +418,57 @@ def test_missing_library_fails_loudly(monkeypatch):
     x, _ = O.synthetic_batch(ocfg)
     with pytest.raises(_lib.HipLibraryError):
         m(x.to(DEV))
+
+
+def test_c2_full_shape_bf16_train_vs_oracle():
+    """BASELINE config 2 at its real shape: ViT-B/16 224^2, B=256 (M = 50,432 token rows), bf16, TRAIN mode (dropout),
+    two blocks (block 0 runs every GEMM at full M with dense gradients; block 1 is the pruned last block), through the
+    engine, against the oracle evaluated on the GPU with torch ops.  This brings the full-size kernels under parity
+    test: the K = 50,432 split-K weight-gradient GEMMs, the persistent many-round forward / dgrad GEMMs (591-2,364
+    tiles) and their split-K tails, the 3,072-item persistent attention backward.  Gates of
+    test_base_width_bf16_engine_vs_oracle: logits 1e-2; each gradient <= max(3e-2, 2 x the spread of valid bf16
+    evaluations: fp32 / fp64 / flash rounding between the same storage points); q/k per block; the whole vector
+    <= max(1e-2, 2 x spread)."""
+    ocfg = O.make_config("base", img=224, batch=256, blocks=2, num_classes=1000)
+    st = O.init_state(ocfg, seed=23)
+    m = _model(ocfg, st, torch.bfloat16).train()
+    x, y = O.synthetic_batch(ocfg)
+    xd, yd = x.to(DEV), y.to(DEV)
+    torch.manual_seed(5)
+    base_seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    torch.manual_seed(5)
+    logits = m(xd)
+    cross_entropy(logits, yd).backward()
+    ours = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    logits = logits.detach()
+    del m
+    torch.cuda.empty_cache()
+    sd = {k: v.to(DEV) for k, v in st.items()}
+    kw = dict(train=True, seed=base_seed)
+    lg_bf, _, g_bf = O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, **kw)
+    assert _rel(logits, lg_bf) < 1e-2, _rel(logits, lg_bf)
+    _, _, g_32 = O.loss_and_grads(sd, xd, yd, ocfg, **kw)
+    valid = [g_bf, O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, dtype=torch.float64, **kw)[2],
+             O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, flash=True, **kw)[2]]
+
+    def err(g, keys):
+        a = torch.cat([g[k].reshape(-1).double() for k in keys])
+        r = torch.cat([g_32[k].reshape(-1).double() for k in keys])
+        return float((a - r).norm() / r.norm())
+
+    groups = {}
+    for k in g_32:
+        if ".query." in k or ".key." in k:
+            groups.setdefault(k.split(".multi_head")[0] + " q/k (all heads)", []).append(k)
+        else:
+            groups[k] = [k]
+    groups["ALL"] = list(g_32)
+    bad, worst = [], []
+    for name, keys in groups.items():
+        e_ours = err(ours, keys)
+        e_ora = max(err(v, keys) for v in valid)
+        worst.append((e_ours / max(e_ora, 1e-9), name, e_ours, e_ora))
+        if e_ours > max(1e-2 if name == "ALL" else 3e-2, 2 * e_ora):
+            bad.append((name, e_ours, e_ora))
+    print("worst error ratios:", sorted(worst)[-4:])
+    assert not bad, bad

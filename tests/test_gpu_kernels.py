@@ -44,9 +44,9 @@ def test_gemm_bf16_exact_integers(akc, bkc, M, N, K):
 @pytest.mark.parametrize("akc,bkc", LAYOUTS)
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 264, 640), (1000, 776, 128), (72, 520, 192),
                                    (2048, 768, 768)])
-def test_gemm_bf16_kernels_exact(monkeypatch, impl, akc, bkc, M, N, K):
-    """Every LDS-DMA kernel variant (VIT_GEMM_IMPL) on ragged M/N tails and 1..12 k-tiles, exact on integers."""
-    monkeypatch.setenv("VIT_GEMM_IMPL", impl)
+def test_gemm_bf16_kernels_exact(libopt, impl, akc, bkc, M, N, K):
+    """Every LDS-DMA kernel variant (option gemm_impl) on ragged M/N tails and 1..12 k-tiles, exact on integers."""
+    libopt("gemm_impl", int(impl))
     g = torch.Generator().manual_seed(M + 5 * N + 11 * K)
     A = _ints((M, K) if akc else (K, M), gen=g)
     B = _ints((N, K) if bkc else (K, N), gen=g)
@@ -61,9 +61,9 @@ def test_gemm_bf16_kernels_exact(monkeypatch, impl, akc, bkc, M, N, K):
 
 @pytest.mark.parametrize("impl", ["2", "4"])
 @pytest.mark.parametrize("split", [3, 7])
-def test_gemm_bf16_kernels_split_k(monkeypatch, impl, split):
+def test_gemm_bf16_kernels_split_k(libopt, impl, split):
     """wgrad form with split-K (incl. an empty last slice: 10 k-tiles over 7 slices) on each kernel variant."""
-    monkeypatch.setenv("VIT_GEMM_IMPL", impl)
+    libopt("gemm_impl", int(impl))
     g = torch.Generator().manual_seed(split)
     M, N, K = 264, 776, 640
     A = _ints((K, M), gen=g)
@@ -77,8 +77,8 @@ def test_gemm_bf16_kernels_split_k(monkeypatch, impl, split):
 
 @pytest.mark.parametrize("variant", ["plain", "bias_relu", "bias_gelu", "aux", "bias_drop_res", "drop_res_f32",
                                      "alpha"])
-def test_gemm_epilogue_kinds_match_general(monkeypatch, variant):
-    """The specialised v4 epilogues are bitwise equal to the general one (VIT_GEMM_EPI_GENERAL=1)."""
+def test_gemm_epilogue_kinds_match_general(libopt, variant):
+    """The specialised v4 epilogues are bitwise equal to the general one (option gemm_epi_general)."""
     torch.manual_seed(7)
     M, N, K = 1000, 776, 256
     x = torch.randn(M, K, device=DEV).bfloat16()
@@ -91,7 +91,7 @@ def test_gemm_epilogue_kinds_match_general(monkeypatch, variant):
           "drop_res_f32": dict(dropout_p=0.3, seed=5, res=res32, ldres=N), "alpha": dict(alpha=0.37)}[variant]
     outs = []
     for general in ("0", "1"):
-        monkeypatch.setenv("VIT_GEMM_EPI_GENERAL", general)
+        libopt("gemm_epi_general", int(general))
         out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         _ops.gemm(x, w, out, M, N, K, K, K, N, **kw)
         outs.append(out)
@@ -149,7 +149,7 @@ def test_gemm_epilogue_bias_relu_dropout_residual(dtype):
 
 
 @pytest.mark.parametrize("B,D", [(3, 256), (5, 768)])
-def test_gemm_row_group_and_rowmod(monkeypatch, B, D):
+def test_gemm_row_group_and_rowmod(libopt, B, D):
     """patch-embed epilogue: rows (b, n) -> b*T + n, + pos[n] (res_rowmod = N); the dedicated wide kind (EPI_PATCH)
     equals the general epilogue bit for bit and leaves the CLS rows alone"""
     torch.manual_seed(1)
@@ -160,7 +160,7 @@ def test_gemm_row_group_and_rowmod(monkeypatch, B, D):
     pos = torch.randn(T, D, device=DEV)
     outs = []
     for general in ("0", "1"):
-        monkeypatch.setenv("VIT_GEMM_EPI_GENERAL", general)
+        libopt("gemm_epi_general", int(general))
         x0 = torch.full((B * T, D), 7.0, device=DEV).bfloat16()
         _ops.gemm(cols, w, x0, B * N, D, K, K, K, D, bias=bias, res=pos, ldres=D, res_rowmod=N, out_group=(N, T))
         outs.append(x0)
@@ -259,7 +259,7 @@ def test_gemm_colsum_part(variant):
 
 
 @pytest.mark.parametrize("variant", ["plain", "bias_relu", "aux", "bias_drop_res"])
-def test_gemm_split_k_tail(monkeypatch, variant):
+def test_gemm_split_k_tail(libopt, variant):
     """A v4 GEMM whose 256x256 tiles leave the last round of the 256 CUs at most half full runs the remaining tile
     rows split-K (M = 23140, N = 768, K = 2304: 91 x 3 tiles = 85 tile rows in whole rounds + 6 tile rows split 8 ways).
     Integer data: outputs and fused column sums equal the unsplit kernel's bit for bit, dropout masks included."""
@@ -276,7 +276,7 @@ def test_gemm_split_k_tail(monkeypatch, variant):
     aux = _ints((M, N), gen=g)
     outs, parts = [], []
     for tail in ("0", "1"):
-        monkeypatch.setenv("VIT_GEMM_TAIL", tail)
+        libopt("gemm_tail", int(tail))
         c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         p = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
         if variant == "aux":
@@ -305,15 +305,15 @@ def _mask4_pack(bits):
 
 
 @pytest.mark.parametrize("variant", ["plain", "bias_relu", "bias_drop_res", "general", "tail", "f32_out", "ragged"])
-def test_gemm_mask4_produce_consume(monkeypatch, variant):
+def test_gemm_mask4_produce_consume(libopt, variant):
     """mask_out = C's mask4 (C as stored > 0; dropout keep bits when the epilogue drops out), and a mask4 aux masks the
     dgrad GEMM exactly as the bf16 tensor it was taken from (ReLU backward, transformer.py:57)."""
     torch.manual_seed(13)
     M, N, K = {"tail": (90 * 256 + 100, 768, 2304), "ragged": (1001, 776, 264)}.get(variant, (1000, 776, 256))
     if variant == "general":
-        monkeypatch.setenv("VIT_GEMM_EPI_GENERAL", "1")
+        libopt("gemm_epi_general", 1)
     if variant == "tail":
-        monkeypatch.setenv("VIT_GEMM_TAIL", "1")
+        libopt("gemm_tail", 1)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
     bias = torch.randn(N, device=DEV)
@@ -350,10 +350,10 @@ def test_gemm_mask4_produce_consume(monkeypatch, variant):
 
 @pytest.mark.parametrize("variant", ["plain", "plain_cs", "bias_relu_mask", "aux_cs", "auxm_cs", "bias_drop_res_mask",
                                      "grouped"])
-def test_gemm_persistent_matches_one_per_item(monkeypatch, variant):
+def test_gemm_persistent_matches_one_per_item(libopt, variant):
     """The wide-epilogue kinds run on a persistent grid (one workgroup per CU looping over its tiles, the next tile's
     first stages staged during the current tile's epilogue).  With more tiles than CUs (ragged last tile row), outputs,
-    masks and fused column sums equal the one-workgroup-per-tile launch (VIT_GEMM_PERSIST=0) bit for bit; integer
+    masks and fused column sums equal the one-workgroup-per-tile launch (option gemm_persist 0) bit for bit; integer
     data makes the plain product exact."""
     g = torch.Generator().manual_seed(17)
     M, N, K = (4200, 4096, 192) if variant == "grouped" else (23 * 256 + 100, 3072, 256)   # 272 / 288 tiles
@@ -365,7 +365,7 @@ def test_gemm_persistent_matches_one_per_item(monkeypatch, variant):
     mask_in = torch.randint(0, 256, (_ops.mask4_bytes(M, N),), generator=g, dtype=torch.uint8).to(DEV)
     results = []
     for persist in ("1", "0", "shared"):      # "shared": VIT_FLAG_SHARED_CUS (the data-parallel backward's launches)
-        monkeypatch.setenv("VIT_GEMM_PERSIST", "0" if persist == "0" else "1")
+        libopt("gemm_persist", 0 if persist == "0" else 1)
         sh = dict(shared_cus=persist == "shared")
         c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         part = torch.empty(_ops.colsum_part_rows(M), N, device=DEV)
@@ -426,7 +426,7 @@ def test_attention_fwd_bwd(dtype, hd, T, amp):
 
 
 @pytest.mark.parametrize("T", [1, 31, 32, 33, 197, 256])
-def test_attention_bwd_fused_matches_split(monkeypatch, T):
+def test_attention_bwd_fused_matches_split(libopt, T):
     """The one-workgroup-per-(image, head) backward (T <= 256) against the split dQ / dK-dV kernels and fp64."""
     torch.manual_seed(T)
     B, H, hd = 2, 3, 64
@@ -435,7 +435,7 @@ def test_attention_bwd_fused_matches_split(monkeypatch, T):
     o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
     d_o = torch.randn(B * T, D, device=DEV).bfloat16()
     fused = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0)
-    monkeypatch.setenv("VIT_ATTN_BWD_SPLIT", "1")
+    libopt("attn_bwd_split", 1)
     split = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0)
     x = qkv.double().requires_grad_(True)
     q, k, v = x.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
@@ -465,13 +465,13 @@ def test_attention_bwd_shared_cus_bitwise(o32):
 
 
 @pytest.mark.parametrize("T", [1, 31, 32, 33, 197, 256])
-def test_attention_fwd_fused_matches_split(monkeypatch, T):
+def test_attention_fwd_fused_matches_split(libopt, T):
     """The one-workgroup-per-(image, head) forward (T <= 256) against the 128-query-tile kernel and fp32."""
     torch.manual_seed(T + 1)
     B, H, hd = 2, 3, 64
     qkv = (torch.randn(B * T, 3 * H * hd, device=DEV) * 0.5).bfloat16()
     of, lf = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
-    monkeypatch.setenv("VIT_ATTN_FWD_SPLIT", "1")
+    libopt("attn_fwd_split", 1)
     osp, lsp = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
     o_ref, lse_ref, _ = _attn_ref(qkv, B, T, H, hd, 8.0)
     ef = (of.float() - o_ref).abs().max().item()

@@ -263,18 +263,18 @@ def test_vit_base_224_bf16_full_size_properties():
 
 
 @pytest.mark.parametrize("dtype,train", [(torch.float32, True), (torch.float32, False), (torch.bfloat16, True)])
-def test_pruned_last_block_matches_all_rows(monkeypatch, dtype, train):
-    """The last block's proj / LN2 / MLP on the B token-0 rows only (VIT_PRUNE_LAST, default) == all B*T rows
-    (VIT_PRUNE_LAST=0): the classifier reads token 0 only (vit.py:80).  Same dropout bits (drawn at the full tensor's
-    indices).  ViT-B width, 2 blocks; fp32 to summation-order rounding, bf16 to a few storage roundings."""
+def test_pruned_last_block_matches_all_rows(dtype, train):
+    """The last block's proj / LN2 / MLP on the B token-0 rows only (engine.prune_last, default) == all B*T rows
+    (prune_last = False): the classifier reads token 0 only (vit.py:80).  Same dropout bits (drawn at the full
+    tensor's indices).  ViT-B width, 2 blocks; fp32 to summation-order rounding, bf16 to a few storage roundings."""
     ocfg = O.make_config("micro", img=64, batch=8, blocks=2)
     ocfg.embedding_size, ocfg.num_heads = 768, 12
     st = O.init_state(ocfg, seed=5)
     x, y = O.synthetic_batch(ocfg)
     out = []
-    for prune in ("1", "0"):
-        monkeypatch.setenv("VIT_PRUNE_LAST", prune)
+    for prune in (True, False):
         m = _model(ocfg, dtype=dtype)
+        m.hip_engine.prune_last = prune
         m.load_state_dict(st)
         m.train(train)
         torch.manual_seed(11)
@@ -290,7 +290,7 @@ def test_pruned_last_block_matches_all_rows(monkeypatch, dtype, train):
 
 
 def test_side_stream_weight_gradients_bitwise_equal():
-    """Weight gradients on the side stream (VIT_CONCURRENT_WGRAD=1) equal the in-order schedule bit for bit."""
+    """Weight gradients on the side stream (engine.concurrent_wgrad) equal the in-order schedule bit for bit."""
     ocfg = O.make_config("micro", img=64, batch=4, blocks=2)
     ocfg.embedding_size, ocfg.num_heads = 128, 2
     st = O.init_state(ocfg, seed=4)

@@ -109,6 +109,13 @@ class Engine:
         self.params = None
         self.ddp_group = None
         self.ddp_enabled = False
+        # dtype the gradient buckets travel in over RCCL (enable_data_parallel(grad_dtype=...)): fp32, or bf16 (half
+        # the ring bytes; the buffer is averaged in bf16 and widened back into the fp32 gradients)
+        self.comm_dtype = torch.float32
+        # when set (bench.py, last timed step): HIP events around the bucket waits at the end of the backward, i.e.
+        # the communication time the backward did not hide ("exposed"); read with comm_exposed_ms()
+        self.time_comm = False
+        self._comm_events = None
         self._works = []
         self._ws = None
         self._ptr_sig = None
@@ -117,13 +124,16 @@ class Engine:
         # callable(family, phase, flop, nbytes) around the hot launches (bench.py's live HIP-event roofline):
         # phase 0 before the launch with its algorithmic FLOPs / HBM bytes, phase 1 after it, same stream
         self.profile_hook = None
-        # weight-gradient GEMMs on a side stream (VIT_CONCURRENT_WGRAD=1).  Off by default: measured on ViT-B/16
-        # B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms/step).
-        self.concurrent_wgrad = os.environ.get("VIT_CONCURRENT_WGRAD", "0") == "1"
-        # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend)
-        self.shared_cus = self.env_shared_cus(False)
+        # weight-gradient GEMMs on a side stream (an attribute for A/B runs and tests).  Off by default: measured on
+        # ViT-B/16 B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms).
+        self.concurrent_wgrad = False
+        # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend;
+        # an attribute, so A/B runs can force either launch mode)
+        self.shared_cus = False
         self._wstream = None
         self._wws = None
+        # the last block's post-attention part on the B token-0 rows only (see forward); False: every row (tests)
+        self.prune_last = True
 
     # ------------------------------------------------------------------------------------------------------------
     # layout
@@ -292,12 +302,6 @@ class Engine:
             self._wstream = torch.cuda.Stream(device=self.device)
         return self._wstream
 
-    @staticmethod
-    def env_shared_cus(default):
-        """VIT_SHARED_CUS=0/1 overrides the launch mode of the backward's persistent kernels (A/B runs)."""
-        v = os.environ.get("VIT_SHARED_CUS")
-        return default if v is None else v == "1"
-
     def _mark(self, fam, phase, flop=0.0, nbytes=0.0):
         h = self.profile_hook
         if h is not None:
@@ -417,8 +421,8 @@ class Engine:
         # The classifier reads token 0 of the last block's output only (vit.py:80), and everything after the last
         # attention is per token: the last block's proj / LN2 / MLP (and their backward) run on the B token-0 rows
         # (rows b*T, row stride T*D; dropout bits drawn at the full tensor's indices) — the same logits, loss and
-        # gradients as computing all B*T rows and discarding the rest.  VIT_PRUNE_LAST=0 computes every row.
-        prune = os.environ.get("VIT_PRUNE_LAST", "1") != "0"
+        # gradients as computing all B*T rows and discarding the rest.  `prune_last = False` computes every row.
+        prune = self.prune_last
         drop_p = DROPOUT_P if training else 0.0
         keep_masks = save and training          # the backward reads the forward's dropout keep bits (mask4)
         for l in range(L):
@@ -441,6 +445,7 @@ class Engine:
             o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
             mk("attn_fwd", 1)
             blk.multi_head.attention_probs = probs
+            blk.multi_head._probs_skipped = probs is None       # a later read warns once (transformer.py)
             # rows of the post-attention part: all M, or (last block, pruned) the B token-0 rows b*T
             pr = prune and l == L - 1
             R, rs = (B, T) if pr else (M, 1)
@@ -491,32 +496,58 @@ class Engine:
     # ------------------------------------------------------------------------------------------------------------
     def _bucket_ready(self, rng, side=None):
         """Launch the all-reduce of one contiguous gradient range (RCCL stream waits on the compute stream, and on
-        the weight-gradient stream `side` when there is one)."""
-        if self.ddp_enabled:
-            a, b = rng
-            if dist.get_backend(self.ddp_group) == "nccl":      # RCCL: native average
-                if side is not None:                          # issued from `side`: the main chain does not wait
-                    side.wait_stream(torch.cuda.current_stream(self.device))
-                    with torch.cuda.stream(side):
-                        w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
-                else:
-                    w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
-                self._works.append((w, None))
-            else:                                             # gloo (CPU tests): sum, scaled after the wait
-                if side is not None:
-                    torch.cuda.current_stream(self.device).wait_stream(side)
-                w = dist.all_reduce(self.G[a:b], op=dist.ReduceOp.SUM, group=self.ddp_group, async_op=True)
-                self._works.append((w, (a, b)))
+        the weight-gradient stream `side` when there is one).  With comm_dtype bf16 the range is first rounded into
+        a bf16 buffer (on the stream that produced it), which is what travels and is averaged."""
+        if not self.ddp_enabled:
+            return
+        a, b = rng
+        bf = self.comm_dtype == torch.bfloat16
+        nccl = dist.get_backend(self.ddp_group) == "nccl"
+        if nccl:                                          # RCCL: native average
+            if side is not None:                          # issued from `side`: the main chain does not wait
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    buf = self.G[a:b].to(torch.bfloat16) if bf else self.G[a:b]
+                    w = dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
+            else:
+                buf = self.G[a:b].to(torch.bfloat16) if bf else self.G[a:b]
+                w = dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.ddp_group, async_op=True)
+            self._works.append((w, rng, buf if bf else None, False))
+        else:                                             # gloo (CPU tests): sum, scaled after the wait
+            if side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(side)
+            buf = self.G[a:b].to(torch.bfloat16) if bf else self.G[a:b]
+            w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.ddp_group, async_op=True)
+            self._works.append((w, rng, buf if bf else None, True))
 
     def _finish_buckets(self):
         if not self._works:
             return
         world = dist.get_world_size(self.ddp_group) if self.ddp_enabled else 1
-        for w, rng in self._works:
-            w.wait()
-            if rng is not None:
-                self.G[rng[0]:rng[1]].mul_(1.0 / world)
+        ev = None
+        if self.time_comm and self.device is not None and self.device.type == "cuda":
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()                      # every backward kernel is enqueued before this point
+        for w, (a, b), buf, scale in self._works:
+            w.wait()                            # nccl: the current stream waits for the collective
+            if buf is not None:
+                self.G[a:b].copy_(buf)          # bf16 average -> fp32 gradients
+                if buf.is_cuda:                 # may have been allocated on the weight-gradient stream
+                    buf.record_stream(torch.cuda.current_stream(buf.device))
+            if scale:
+                self.G[a:b].mul_(1.0 / world)
+        if ev is not None:
+            ev[1].record()
+        self._comm_events = ev
         self._works = []
+
+    def comm_exposed_ms(self):
+        """Milliseconds the compute stream spent, after the last backward kernel, waiting for the gradient
+        all-reduce of the most recent backward with time_comm set (None if not measured).  Synchronizes."""
+        if self._comm_events is None:
+            return None
+        self._comm_events[1].synchronize()
+        return self._comm_events[0].elapsed_time(self._comm_events[1])
 
     def backward(self, tape, dlogits):
         D, T, N, H, hd, L, dt = self.D, self.T, self.N, self.H, self.hd, self.L, self.dtype
@@ -527,6 +558,15 @@ class Engine:
         mk = self._mark
         # decided at backward time: the reference calls zero_grad(set_to_none=True) between forward and backward
         beta = self._attach_grads()
+        # Accumulating into existing .grad (no zero_grad between backwards) with `register_hook` hooks present:
+        # autograd applies such a hook to THIS backward's gradient only, then accumulates.  Keep the old gradients
+        # aside, let the kernels overwrite the buffer with the increment (beta 0), and let run_param_hooks() hook
+        # the increment and add the old values back (old + increment is the same single fp32 rounding the beta=1
+        # epilogues do, so hook-free parameters keep their bits).
+        self._acc_old = None
+        if beta == 1.0 and any(p.requires_grad and p._backward_hooks for p, _ in self.grad_views):
+            self._acc_old = self.G.clone()
+            beta = 0.0
         req = {k: any(p.requires_grad for p in ps) for k, ps in self.owners.items()}
         # the backward stops at the first block below which nothing (parameters, input image) needs a gradient
         below = tape.x_grad or any(req[k] for k in ("conv_w", "conv_b", "cls", "pos"))
@@ -683,8 +723,12 @@ class Engine:
 
     def run_param_hooks(self):
         """Parameter hooks after the fused backward (autograd's AccumulateGrad never runs for these parameters):
-        `register_hook` hooks see the gradient and may replace it, then `register_post_accumulate_grad_hook`
-        hooks run on the parameter — each once per backward, in registration order."""
+        `register_hook` hooks see this backward's gradient and may replace it, then
+        `register_post_accumulate_grad_hook` hooks run on the parameter — each once per backward, in registration
+        order.  When the backward accumulated into existing gradients, the buffer holds the increment here
+        (backward() set `_acc_old`): the hooks see the increment, then the previous gradients are added back."""
+        old = getattr(self, "_acc_old", None)
+        self._acc_old = None
         for p, gv in self.grad_views:
             if not p.requires_grad or p.grad is None:
                 continue
@@ -697,6 +741,11 @@ class Engine:
                         g = r
                 if g is not p.grad:
                     p.grad.copy_(g)
+        if old is not None:
+            self.G.add_(old)
+        for p, gv in self.grad_views:
+            if not p.requires_grad or p.grad is None:
+                continue
             post = getattr(p, "_post_accumulate_grad_hooks", None)
             if post:
                 for fn in post.values():

@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 F32, BF16, MASK4 = 0, 1, 2
 FLAG_SHARED_CUS = 1          # VIT_FLAG_SHARED_CUS (vit_hip.h)
@@ -52,6 +52,8 @@ _P, _I64, _I32, _F, _U32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctyp
 _SIGS = {
     "vit_abi_version": (ctypes.c_int, []),
     "vit_last_error": (ctypes.c_char_p, []),
+    "vit_set_option": (ctypes.c_int, [ctypes.c_char_p, _I64]),
+    "vit_get_option": (_I64, [ctypes.c_char_p]),
     "vit_gemm_workspace_bytes": (_I64, [ctypes.POINTER(GemmDesc)]),
     "vit_gemm": (ctypes.c_int, [ctypes.POINTER(GemmDesc), _P]),
     "vit_gemm_split_k_hint": (ctypes.c_int, [_I64, _I64, _I64, _I32]),
@@ -120,3 +122,34 @@ def check(rc, what):
 def call(name, *args):
     lib = load()
     check(getattr(lib, name)(*args), name)
+
+
+def set_option(name, value):
+    """vit_set_option (vit_hip.h): process-wide launch option of the library (kernel-variant choice for A/B runs and
+    tests; defaults are the shipped configuration).  Returns the previous value."""
+    lib = load()
+    prev = lib.vit_get_option(name.encode())
+    check(lib.vit_set_option(name.encode(), int(value)), f"vit_set_option({name!r})")
+    return prev
+
+
+def get_option(name):
+    v = load().vit_get_option(name.encode())
+    if v == -(1 << 63):
+        raise KeyError(f"unknown libvit_hip option {name!r}")
+    return v
+
+
+class option:
+    """Context manager: `with _lib.option("gemm_persist", 0): ...` sets an option and restores it on exit."""
+
+    def __init__(self, name, value):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.prev = set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.prev)
+        return False

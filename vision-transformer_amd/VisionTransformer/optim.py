@@ -21,42 +21,50 @@ class FusedAdamW(torch.optim.Optimizer):
     """Step bookkeeping stays on the host: each group's per-parameter 'step' entries are 0-d views of ONE CPU
     tensor (torch AdamW's state format, so `state_dict()` / `load_state_dict()` interchange with it), advanced by a
     single in-place add per step, with a host-side mirror of the counts for the bias corrections — no per-parameter
-    `.item()` or `+= 1` on the step path.  Device chunk tables are cached per group and keyed on every pointer they
-    hold (param, grad, shadow, exp_avg, exp_avg_sq), and hold references to those tensors."""
+    `.item()` or `+= 1` on the step path.  Device chunk tables are cached per (group, step-count class) and hold
+    references to every tensor whose pointer they carry.  A cached table is reused while the optimizer's version
+    (bumped by load_state_dict / add_param_group / fresh state) is unchanged and every parameter still has the very
+    same .grad tensor object (identity checks, no per-step pointer signature): the engine's gradient views are new
+    objects whenever its buffers (and with them the shadows) are rebuilt.  After `p.data = other` on a parameter that
+    no engine owns, call `invalidate()`."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, grad_scale=1.0):
         if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError("invalid AdamW hyper-parameters")
+        self._version = 0
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.grad_scale = grad_scale
         self._tables = {}
-        self._steps = {}          # group index -> (steps tensor [n] f32 CPU, host list of ints)
+        self._steps = {}          # group index -> (params list, steps tensor [n] f32 CPU, host list of ints)
+
+    def invalidate(self):
+        """Drop every cached chunk table and step mirror (parameters re-pointed outside any engine)."""
+        self._version += 1
+        self._tables = {}
+        self._steps = {}
 
     # ---- step counters ------------------------------------------------------------------------------------------
     def _step_state(self, gi, group):
         ent = self._steps.get(gi)
         ps = group["params"]
-        if ent is not None and len(ent[1]) == len(ps):
-            return ent
+        if ent is not None and len(ent[0]) == len(ps) and all(a is b for a, b in zip(ent[0], ps)):
+            return ent[1], ent[2]
         host = [int(float(self.state[p]["step"])) if "step" in self.state[p] else 0 for p in ps]
         buf = torch.tensor(host, dtype=torch.float32)
         for i, p in enumerate(ps):
             if "step" in self.state[p]:
                 self.state[p]["step"] = buf[i]
-        ent = (buf, host)
-        self._steps[gi] = ent
-        return ent
+        self._steps[gi] = (list(ps), buf, host)
+        return buf, host
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
-        self._tables = {}         # the moments are new tensors: every cached chunk table is stale
-        self._steps = {}
+        self.invalidate()         # the moments are new tensors: every cached chunk table is stale
 
-    def _signature(self, plist):
-        st = self.state
-        return tuple((p.data_ptr(), p.grad.data_ptr(),
-                      shadow_of(p) is not None and shadow_of(p).data_ptr(),
-                      st[p]["exp_avg"].data_ptr(), st[p]["exp_avg_sq"].data_ptr()) for p in plist)
+    def add_param_group(self, param_group):
+        super().add_param_group(param_group)
+        if hasattr(self, "_tables"):
+            self.invalidate()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -83,7 +91,7 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     fresh = True
             if fresh:
-                self._steps.pop(gi, None)
+                self.invalidate()
             buf, host = self._step_state(gi, group)
             # advance the counters: one in-place add on the shared tensor, host mirror in Python ints
             if len(idx) == len(ps_all):
@@ -96,13 +104,15 @@ class FusedAdamW(torch.optim.Optimizer):
                 by_step.setdefault(host[i], []).append(ps_all[i])
             b1, b2 = group["betas"]
             for t, ps in by_step.items():
-                shadows = [shadow_of(p) for p in ps]
-                sdt = next((s.dtype for s in shadows if s is not None), torch.float32)
-                shadows = [s if (s is not None and s.dtype == sdt) else None for s in shadows]
-                key = (gi, len(by_step) == 1 or t)
-                sig = (self._signature(ps), sdt)
+                # one table for the whole group while every parameter has the same step count, else one per count
+                key = (gi, "all") if len(by_step) == 1 else (gi, "t", t)
                 tab = self._tables.get(key)
-                if tab is None or tab[0] != sig:
+                if tab is not None and not self._table_valid(tab, ps):
+                    tab = None
+                if tab is None:
+                    shadows = [shadow_of(p) for p in ps]
+                    sdt = next((s.dtype for s in shadows if s is not None), torch.float32)
+                    shadows = [s if (s is not None and s.dtype == sdt) else None for s in shadows]
                     entries = [(p, p.grad, self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"], s)
                                for p, s in zip(ps, shadows)]
                     for p, g, m, v, _ in entries:
@@ -110,12 +120,22 @@ class FusedAdamW(torch.optim.Optimizer):
                             if not tt.is_contiguous():
                                 raise RuntimeError("FusedAdamW: non-contiguous grad/state")
                     dev_tab, n = _ops.build_chunk_table(entries, ps[0].device)
-                    tab = (sig, dev_tab, n, entries)          # entries keep every tabled tensor alive
+                    # entries keep every tabled tensor alive; the raw shadow list is what the identity check compares
+                    tab = (self._version, list(ps), [p.grad for p in ps], [shadow_of(p) for p in ps], dev_tab, n,
+                           sdt, entries)
                     self._tables[key] = tab
-                _, dev_tab, n, _ = tab
+                dev_tab, n, sdt = tab[4], tab[5], tab[6]
                 _ops.adamw(dev_tab, n, group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** t,
                            1.0 - b2 ** t, self.grad_scale, sdt)
         return loss
+
+    def _table_valid(self, tab, ps):
+        """Same optimizer version, same parameters, and every parameter still holds the same .grad tensor object as
+        when the table was built (identity, not pointers: a few hundred `is` tests per step).  The engine's shadows
+        change only when it rebuilds its buffers, and then every gradient view is a new object too."""
+        ver, tps, grads = tab[0], tab[1], tab[2]
+        return (ver == self._version and len(tps) == len(ps)
+                and all(a is b and a.grad is g for a, b, g in zip(tps, ps, grads)))
 
 
 class _XentFn(torch.autograd.Function):

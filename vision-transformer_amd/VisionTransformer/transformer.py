@@ -35,13 +35,36 @@ class Head(nn.Module):
         return Fh.head_attention(x, self.query.weight, self.key.weight, self.value.weight)
 
 
+_PROBS_WARNED = False
+
+
 class MultiHeadAttention(nn.Module):
     def __init__(self, num_heads, head_size, n_embd, block_size, dropout=0.2):
         super().__init__()
         self.heads = nn.ModuleList([Head(head_size, n_embd, block_size) for _ in range(num_heads)])
         self.proj = nn.Linear(n_embd, n_embd)
-        self.attention_probs = None
+        self._attention_probs = None
+        self._probs_skipped = False     # set by the fused engine when it ran without storing probabilities
         self.dropout = nn.Dropout(dropout)
+
+    @property
+    def attention_probs(self):
+        """[B, H, T, T] attention probabilities of the last forward (transformer.py:48).  The fused whole-model
+        forward stores them only with `model.store_attention_probs = True` (477 MB per layer at ViT-B/16 B=256);
+        reading them after a fused forward without the flag returns None and warns once."""
+        global _PROBS_WARNED
+        if self._attention_probs is None and self._probs_skipped and not _PROBS_WARNED:
+            _PROBS_WARNED = True
+            import warnings
+            warnings.warn("MultiHeadAttention.attention_probs is None: the fused VisionTransformer forward keeps the "
+                          "attention probabilities only when `model.store_attention_probs = True` (the reference "
+                          "always stores them, transformer.py:48)", UserWarning, stacklevel=2)
+        return self._attention_probs
+
+    @attention_probs.setter
+    def attention_probs(self, value):
+        self._attention_probs = value
+        self._probs_skipped = False
 
     def forward(self, x):
         pairs = [head(x) for head in self.heads]

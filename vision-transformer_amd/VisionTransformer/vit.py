@@ -95,18 +95,23 @@ class VisionTransformer(nn.Module):
             self._engine = Engine(self)
         return self._engine
 
-    def enable_data_parallel(self, group=None, force=False):
+    def enable_data_parallel(self, group=None, force=False, grad_dtype=torch.float32):
         """Average gradients across the process group with RCCL, bucketed per block, overlapped with backward.
-        `force` keeps the all-reduce path on even for a world of one rank (tests the collective on one GPU)."""
+        `force` keeps the all-reduce path on even for a world of one rank (tests the collective on one GPU).
+        `grad_dtype=torch.bfloat16` sends each bucket as bf16 (half the xGMI ring bytes): the fp32 gradients are
+        rounded to bf16, averaged in bf16 and widened back; master weights and optimizer state stay fp32."""
         import torch.distributed as dist
         if not dist.is_initialized():
             raise RuntimeError("enable_data_parallel: torch.distributed is not initialised")
+        if grad_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("enable_data_parallel: grad_dtype must be torch.float32 or torch.bfloat16")
         eng = self.hip_engine
         eng.ddp_group = group
+        eng.comm_dtype = grad_dtype
         eng.ddp_enabled = bool(force) or dist.get_world_size(group) > 1
         # RCCL's all-reduce kernels run on the GPU beside the backward: the backward's kernels then launch one
         # workgroup per item instead of a persistent one-per-CU grid (VIT_FLAG_SHARED_CUS, vit_hip.h)
-        eng.shared_cus = eng.env_shared_cus(eng.ddp_enabled and dist.get_backend(group) == "nccl")
+        eng.shared_cus = eng.ddp_enabled and dist.get_backend(group) == "nccl"
         return self
 
     # the engine holds a weakref to its model and views of the parameters: never copy or pickle it (a deep copy or

@@ -842,10 +842,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         const int qs = (it - 2) * 32;
         store_rows64(dQs + ((it - 2) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
       }
-#ifndef VIT_AB_NOPAIR
       if (kact && it < nqb) pair(it);
-#endif
-#ifndef VIT_AB_NODQ
       if (it >= 1) {
         const int qb = it - 1;
         const bf16_t* dS = dSt + (qb & 1) * DST;
@@ -860,7 +857,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
         st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * 64 + dd * 16 + 4 * (lane >> 4), v4);
       }
-#endif
       if (more && it >= 1) {
         const int pc = (it - 1) * 4 + (wave & 3);
         if (wave < 4) dma_piece(qkv, nb_ * Tn, ld, nh_ * HD, Tn, Qs, pc, lane);
@@ -876,30 +872,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       const int qs = (nqb - 1) * 32;
       store_rows64(dQs + ((nqb - 1) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
     }
-#ifdef VIT_BWD_STAGED_DKDV
-    // K and dS^T are dead (the last dQ block ran before the final barrier): dK / dV images there, full-row stores
-    if (kact) {
-#pragma unroll
-      for (int db = 0; db < 2; ++db) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
-                        dk[db][4 * g + 3] * scale};
-          float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
-          st4<bf16_t>(Ks + key * 64 + db * 32 + 8 * g + 4 * hf, a);
-          st4<bf16_t>(dSt + key * 64 + db * 32 + 8 * g + 4 * hf, c);
-        }
-      }
-    }
-    lds_barrier();
-    store_rows64(Ks, Tp, Tn, dqkv + b * Tn * ld + D + h * HD, ld, tid, 512);
-    store_rows64(dSt, Tp, Tn, dqkv + b * Tn * ld + 2 * D + h * HD, ld, tid, 512);
-    lds_barrier();                                    // images read before the next item's DMA overwrites them
-    if (more) {
-      dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
-      if (!dglob) dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
-    }
-#else
     // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K and O
     if (more) {
       dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
@@ -920,7 +892,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         }
       }
     }
-#endif
   }
 }
 
@@ -1044,7 +1015,7 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && probs == nullptr) {
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
-    if (T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_FWD_SPLIT")) {
+    if (T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_FWD_SPLIT)) {
 #define FWD(NK) \
   attn_fwd_fused<NK><<<(unsigned)(B * H), NK * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, scale)
       switch ((int)((T + 31) / 32)) {
@@ -1089,7 +1060,7 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
   hipStream_t s = VIT_STREAM(stream);
   const int64_t rows = B * T * H;
   const unsigned dgrid = (unsigned)std::min<int64_t>((rows * 8 + 255) / 256, 16384);
-  if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !getenv("VIT_ATTN_BWD_SPLIT")) {
+  if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_BWD_SPLIT)) {
     // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid
     const int64_t items = B * H;
     const float* dl = nullptr;             // without o32 the kernel computes delta from the bf16 O itself
@@ -1099,7 +1070,7 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
     }
     // persistent: one workgroup per CU; VIT_FLAG_SHARED_CUS: one per item (no cross-item prefetch, any free CU)
     int64_t grid = (flags & VIT_FLAG_SHARED_CUS) ? items : std::min<int64_t>(items, vit_cu_count());
-    if (const char* e = getenv("VIT_ATTN_BWD_GRID")) grid = std::max<int64_t>(1, std::min<int64_t>(items, atoll(e)));
+    if (const int64_t gopt = vit::opt(vit::OPT_ATTN_BWD_GRID)) grid = std::max<int64_t>(1, std::min<int64_t>(items, gopt));
 #define BWD(NQ)                                                                                                  \
   attn_bwd_fused<NQ><<<(unsigned)grid, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \
                                                     dl, (bf16_t*)dqkv, T, H, items, scale)

@@ -100,6 +100,15 @@ void colsum_parts_launch(const void* x, int64_t ldx, int dtype, int64_t rows, in
                          float* part, hipStream_t s);
 }  // namespace vit
 
+// Launch options of vit_set_option (vit_hip.h), read by the host-side launchers.
+namespace vit {
+enum Opt : int {
+  OPT_GEMM_IMPL = 0, OPT_GEMM_TAIL, OPT_GEMM_TAIL_MIN_KT, OPT_SPLITK_MIN_KT, OPT_GEMM_GROUP_M, OPT_GEMM_EPI_GENERAL,
+  OPT_GEMM_PERSIST, OPT_ATTN_FWD_SPLIT, OPT_ATTN_BWD_SPLIT, OPT_ATTN_BWD_GRID, OPT_LN16, OPT_LN_AL, OPT_COUNT
+};
+int64_t opt(Opt o);
+}  // namespace vit
+
 // Compute units of the current device (256 on MI355X), queried once per device.
 static inline int64_t vit_cu_count() {
   static int cache[64] = {0};

@@ -12,8 +12,6 @@
 // f32 path: 64x64x16 tile, v_mfma_f32_32x32x2_f32 (bit-for-bit an fp32 fma chain) — exact-fp32 parity path.
 // Split-K (wgrad: reduction over B*T rows): fp32 slabs per K-slice, then a deterministic reduce that applies the
 // same epilogue.
-#include <stdlib.h>
-
 #include "vit_common.h"
 
 namespace {
@@ -482,9 +480,6 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_v2(GemmArgs g, EpiParams e, 
       const int64_t i = i0 + wm * 64 + x * 16 + (lane & 15);
       const int64_t j = j0 + wn * 64 + y * 16 + 4 * (lane >> 4);
       float v[4] = {acc[x][y][0], acc[x][y][1], acc[x][y][2], acc[x][y][3]};
-#ifdef VIT_GEMM_NOEPI
-      if (v[0] != 1234.5f) continue;   // diagnostic build: no stores (acc stays live)
-#endif
       if (g.ws) slab_store4(g.ws + (int64_t)blockIdx.y * g.M * g.N, g.M, g.N, i, j, v);
       else epilogue4<TO>(e, i, j, v);
     }
@@ -624,35 +619,9 @@ VIT_DEV uint32_t v4_epi_row(const EpiParams& e, const GemmArgs& g, int64_t i, in
   return pos;
 }
 
-template <bool KC>
-VIT_DEV void dma_offsets4(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int wave, int lane, uint32_t (&off)[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int ii = wave * 2 + i;            // 16 pieces of 1 KiB per half-tile, 2 per wave
-    int64_t gr, gk;
-    if (KC) {
-      const int r = ii * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ (r & 7);
-      gr = r0 + r;
-      gk = k0 + c * 8;
-    } else {
-      const int kr = ii * 4 + (lane >> 4);
-      const int c = (lane & 15) ^ swz_rs(kr);
-      gk = k0 + kr;
-      gr = r0 + c * 8;
-    }
-    const int64_t eoff = KC ? gr * ld + gk : gk * ld + gr;
-    off[i] = gr < rows ? (uint32_t)(eoff * 2) : OOB;
-  }
-}
-
-// V4_GLDS (default; -DV4_BUFFER_LDS for the buffer form): the same pieces by global_load_lds_dwordx4 (per-lane 64-bit
-// source address) instead of buffer_load ... lds; rows past the operand are clamped to its last row (their products
-// land in output rows / columns that are never stored).  Measured 2-4% faster on the k-contiguous-A shapes (QKV fwd
-// 218 -> 209 us, fc2 fwd 255 -> 245 us), neutral on the weight gradients (tools/r2l.sh).
-#if !defined(V4_BUFFER_LDS) && !defined(V4_GLDS)
-#define V4_GLDS 1
-#endif
+// The pieces of one half-tile, 2 per wave, by global_load_lds_dwordx4 (per-lane 64-bit source address; the buffer
+// form, buffer_load ... lds, measured 2-4% slower on the k-contiguous-A shapes, neutral on the weight gradients); rows
+// past the operand are clamped to its last row (their products land in output rows / columns that are never stored).
 template <bool KC>
 VIT_DEV void dma_offsets4g(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int wave, int lane, uint32_t (&off)[2]) {
 #pragma unroll
@@ -695,13 +664,6 @@ VIT_DEV void dma_half_g(const char* base, const uint32_t (&off)[2], uint32_t sof
       "global_load_lds_dwordx4 %1, off" ::"v"(p0), "v"(p1), "s"(lds)
       : "memory", "m0");
 #pragma clang diagnostic pop
-}
-
-VIT_DEV void dma_half(__amdgpu_buffer_rsrc_t rs, const uint32_t (&off)[2], uint32_t soff, bf16_t* half, int wave) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        rs, (__attribute__((address_space(3))) void*)(half + (wave * 2 + i) * 512), 16, off[i], soff, 0, 0);
 }
 
 // LDS ring of the v4 k-loop: V4_SLOTS half-tile images (16 KiB each); stage s (k-tile s/4, half A0/B0/B1/A1) lands in
@@ -756,26 +718,6 @@ VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const
   __builtin_amdgcn_s_setprio(0);
 }
 
-// Diagnostic build only (-DVIT_GEMM_STAMPS): wave 0 of every v4 workgroup records s_memtime at fixed points into a
-// buffer of its own (nothing in the kernel reads it back; no output depends on it) — MI355X_MICROARCH.md 'DVFS
-// give-back' (6).  Read with vit_gemm_debug_stamps().
-// The kernel accumulates, per workgroup and in registers, the cycles spent in each interval (V4_ACC(K): slot K += now -
-// previous stamp) and stores the 8 sums at its end: 0 k-loop, 1 next-tile stage issue, 2 epilogue, 3 restage + wait,
-// 4 loop-top barrier, 5 first prologue, 6 items processed, 7 tail (last epilogue to all stores retired).
-#ifdef VIT_GEMM_STAMPS
-__device__ unsigned long long vit_stamps[16384 * 8];
-#define V4_STAMP(K) do {} while (0)
-#define V4_ACC(K)                                                                              \
-  do {                                                                                         \
-    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                              \
-    st_acc_[K] += now_ - st_last_;                                                             \
-    st_last_ = now_;                                                                           \
-  } while (0)
-#else
-#define V4_STAMP(K) do {} while (0)
-#define V4_ACC(K) do {} while (0)
-#endif
-
 // Row-contiguous epilogue through LDS, one 128-row half of the tile per pass: the fragment layout (16 rows x 32 B
 // per store instruction) becomes 1 row x 256 columns per wave instruction, so output stores and residual / mask
 // loads are full-line.  Image: [128][256] fp32, 16-B chunk index XOR (row & 15) -> conflict-free b128 writes
@@ -814,7 +756,6 @@ VIT_DEV void v4_epilogue(const EpiParams& e, const GemmArgs& g, const f32x4 (&ac
       }
   }
   __syncthreads();                                        // every wave's k-loop LDS reads are done, no DMA pending
-  V4_STAMP(3);
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
 #pragma unroll
@@ -839,9 +780,6 @@ VIT_DEV void v4_epilogue(const EpiParams& e, const GemmArgs& g, const f32x4 (&ac
       const int row = wave * 16 + rr;
       float v[4] = {rv[rr][0], rv[rr][1], rv[rr][2], rv[rr][3]};
       const int64_t i = i0 + mh * 128 + row, j = j0 + 4 * lane;
-#ifdef VIT_GEMM_NOEPI
-      if (v[0] != 1234.5f) continue;
-#endif
       const uint32_t nib = v4_epi_row<TO, KIND, ACT>(e, g, i, j, b4, v, has_pre ? pre[mh][rr] : make_uint2(0u, 0u));
       if (mk_on) {
         mword |= (nib & 0xfu) << (8 * (rr & 3));
@@ -858,7 +796,6 @@ VIT_DEV void v4_epilogue(const EpiParams& e, const GemmArgs& g, const f32x4 (&ac
     }
     if (mh == 0) __syncthreads();
   }
-  V4_STAMP(4);
   if (cs_on) {
     // per-lane sums of the wave's 32 rows -> LDS -> the 8 wave sums added in wave order: one row of csum per tile
     __syncthreads();
@@ -972,11 +909,7 @@ VIT_DEV uint32_t v4_epi_row8(const EpiParams& e, int64_t i, int64_t j, bf16_t* c
   uint32_t w[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) w[q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
-#ifdef VIT_EPI_NOSTORE   // ablation build: everything but the output store (values kept live)
-  asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
-#else
   *reinterpret_cast<uint4*>(cp) = make_uint4(w[0], w[1], w[2], w[3]);
-#endif
   if (MK || CS) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {                                 // as stored
@@ -1067,9 +1000,6 @@ VIT_DEV void v4_epilogue_w(const EpiParams& e, const f32x4 (&acc)[2][2][4][2], f
       const int64_t i = rbase + rr;
       const int sh = 8 * (rr & 3);
       uint32_t bits = 0u;
-#ifdef VIT_GEMM_NOEPI
-      if (v[0] != 1234.5f) continue;
-#endif
       if (jok && rr < rows_left) {
         bf16_t* cp = cbase + (uint32_t)(rr * (int)e.ldc + 8 * l);
         bits = v4_epi_row8<KIND, ACT, MK, CS>(e, i, j, cp, b8, v, has_pre ? pre[k & 1][p] : make_uint4(0u, 0u, 0u, 0u),
@@ -1093,7 +1023,6 @@ VIT_DEV void v4_epilogue_w(const EpiParams& e, const f32x4 (&acc)[2][2][4][2], f
         }
       }
     }
-    V4_STAMP(3 + k);
     if (k < 3) V4_LDS_BARRIER();                        // the next pass overwrites the image
   }
 #undef V4W_PRE
@@ -1178,9 +1107,6 @@ VIT_DEV void v4_epilogue_d(const EpiParams& e, f32x4 (&acc)[2][2][4][2], float* 
         float v[8] = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
         const int64_t i = rbase + 16 * x, j = j0 + nh * 128 + wc * 32 + cq;
         uint32_t bits = 0u;
-#ifdef VIT_GEMM_NOEPI
-        if (v[0] != 1234.5f) continue;
-#endif
         if (i < e.m && j < e.n) {
           // EPI_PATCH: output row (i / G) * Gs + i % G (32-bit: the host bounds m)
           const int64_t orow = KIND == EPI_PATCH ? (int64_t)((int)i / (int)e.grp) * e.grp_stride + (int)i % (int)e.grp : i;
@@ -1271,17 +1197,10 @@ VIT_DEV void v4_item(const GemmArgs& g, int64_t item, int64_t& tm, int64_t& tn, 
 template <bool AKC, bool BKC>
 VIT_DEV void v4_offsets(const GemmArgs& g, int64_t i0, int64_t j0, int64_t k0, int wave, int lane, uint32_t (&oa0)[2],
                         uint32_t (&oa1)[2], uint32_t (&ob0)[2], uint32_t (&ob1)[2]) {
-#ifdef V4_GLDS
   dma_offsets4g<AKC>(g.lda, g.M, i0, k0, wave, lane, oa0);
   dma_offsets4g<AKC>(g.lda, g.M, i0 + 128, k0, wave, lane, oa1);
   dma_offsets4g<BKC>(g.ldb, g.N, j0, k0, wave, lane, ob0);
   dma_offsets4g<BKC>(g.ldb, g.N, j0 + 128, k0, wave, lane, ob1);
-#else
-  dma_offsets4<AKC>(g.lda, g.M, i0, k0, wave, lane, oa0);
-  dma_offsets4<AKC>(g.lda, g.M, i0 + 128, k0, wave, lane, oa1);
-  dma_offsets4<BKC>(g.ldb, g.N, j0, k0, wave, lane, ob0);
-  dma_offsets4<BKC>(g.ldb, g.N, j0 + 128, k0, wave, lane, ob1);
-#endif
 }
 
 // Persistent form (the wide-epilogue kinds: bf16 output, fast epilogue; the host launches one workgroup per CU): a
@@ -1311,30 +1230,18 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   const int64_t step = (nwg - xcd + 7) / 8;              // workgroups on this XCD
   int64_t item = lo + orig / 8;
   if (item >= hi) return;
-#ifdef VIT_GEMM_STAMPS
-  unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long st_last_ = __builtin_amdgcn_s_memtime();
-#endif
   int64_t tm, tn, sidx;
   v4_item(g, item, tm, tn, sidx);
   int64_t i0 = tm * 256, j0 = tn * 256;
   const int64_t nkt = g.K / BK;
   int nk = (int)max((int64_t)0, min(nkt, (sidx + 1) * g.kt_per_split) - sidx * g.kt_per_split);
-#ifndef V4_GLDS
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.a, a_bytes);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.b, b_bytes);
-#endif
   const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
   const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
   uint32_t oa0[2], oa1[2], ob0[2], ob1[2];
   v4_offsets<AKC, BKC>(g, i0, j0, sidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
-#ifdef V4_GLDS
   const char* pa_ = (const char*)g.a;
   const char* pb_ = (const char*)g.b;
 #define V4_DMA(R, P, OFF, SOFF, DST) dma_half_g(P, OFF, SOFF, DST, wave)
-#else
-#define V4_DMA(R, P, OFF, SOFF, DST) dma_half(R, OFF, SOFF, DST, wave)
-#endif
 
   // stage s -> (k-tile s>>2, half order A0, B0, B1, A1) in LDS slot s % V4_SLOTS
 #define V4_SLOT(S) (smem4 + ((S) % V4_SLOTS) * HALF)
@@ -1357,10 +1264,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 
   f32x4 acc[2][2][4][2];
   bf16x8_t af[4][2], b0f[2][2], b1f[2][2];
-  V4_ACC(5);
   while (true) {
     __builtin_amdgcn_s_barrier();
-    V4_ACC(4);
     if (wr == 1) __builtin_amdgcn_s_barrier();            // group 1 runs one barrier behind group 0
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -1373,7 +1278,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 
     // One phase f = 4t + r.  STEADY: the k-tiles before the last two, where every phase issues its DMA stage and the
     // retiring wait is the constant vmcnt(2 * (LEAD - 2)) — no per-phase branches (the tail's counts are computed).
-#ifndef VIT_V4_NODMA
 #define V4_PHASE_DMA(F, STEADY)                                                                  \
   do {                                                                                           \
     if (STEADY) {                                                                                \
@@ -1384,17 +1288,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
       wait_stage_retired(min(V4_LEAD - 2, nstage - 1 - ((F) + 2)));                              \
     }                                                                                            \
   } while (0)
-#else
-#define V4_PHASE_DMA(F, STEADY) do {} while (0)
-#endif
-#ifdef VIT_V4_NOMFMA
-#define V4_PHASE_MFMA(R)                                                                         \
-  do {                                                                                           \
-    if ((R) == 0) { asm volatile("" ::"v"(af[0][0]), "v"(af[3][1]), "v"(b0f[0][0]), "v"(b0f[1][1])); } \
-    else if ((R) == 1) { asm volatile("" ::"v"(b1f[0][0]), "v"(b1f[1][1])); }                    \
-    else if ((R) == 2) { asm volatile("" ::"v"(af[0][0]), "v"(af[3][1])); }                       \
-  } while (0)
-#else
 #define V4_PHASE_MFMA(R)                                                                         \
   do {                                                                                           \
     if ((R) == 0) mfma_quadrant(acc[0][0], af, b0f);                                             \
@@ -1402,7 +1295,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     else if ((R) == 2) mfma_quadrant(acc[1][1], af, b1f);                                        \
     else mfma_quadrant(acc[1][0], af, b0f);                                                      \
   } while (0)
-#endif
 #define V4_PHASE(T, R, STEADY)                                                                   \
   do {                                                                                           \
     const int f_ = 4 * (T) + (R);                                                                \
@@ -1441,7 +1333,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 #undef V4_PHASE_MFMA
 #undef V4_PHASE_DMA
     if (wr == 0) __builtin_amdgcn_s_barrier();            // balance group 1's extra barrier
-    V4_ACC(0);
 
     // next item: its first stages go out now (slots 0-3), ahead of this tile's epilogue
     const int64_t next = item + step;
@@ -1457,24 +1348,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
       npre = min(V4_LEAD, 4 * nnk);
       for (int s = 0; s < npre; ++s) V4_STAGE(s);
     }
-    V4_ACC(1);
 
-#if defined(VIT_V4_DIRECT_EPI)
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-      for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-          for (int y = 0; y < 2; ++y) {
-            const int64_t i = i0 + mh * 128 + wr * 64 + x * 16 + (lane & 15);
-            const int64_t j = j0 + nh * 128 + wc * 32 + y * 16 + 4 * (lane >> 4);
-            const f32x4 a = acc[mh][nh][x][y];
-            float v[4] = {a[0], a[1], a[2], a[3]};
-            v4_epi_row<TO, EPI_GENERAL, 0>(e, g, i, j, v, v);
-          }
-#else
     // The epilogue's per-lane address arithmetic is loop-invariant; hoisted out of the persistent loop it stayed live
     // across the k-loop and spilled.  An opaque copy of tid makes the compiler recompute it per tile (a few dozen VALU).
     int tid_e = tid;
@@ -1491,11 +1365,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
       if (gi.ws) gi.ws += sidx * g.M * g.N;                 // this K-slice's fp32 slab (EPI_SLAB)
       v4_epilogue<TO, KIND, 0>(e, gi, acc, smem4, tid_e, i0, j0, tm);
     }
-#endif
-    V4_ACC(2);
-#ifdef VIT_GEMM_STAMPS
-    st_acc_[6] += 1;
-#endif
     if (!have_next) break;
     // advance: the rest of the next item's prologue (its stages 4..LEAD-1 land in slots the image used)
     item = next;
@@ -1509,19 +1378,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     // stages 0..LEAD-1 went out before the epilogue; its loads and stores are younger, so retiring stages 0 and 1
     // waits for them too (vmcnt counts in order): wait for everything
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    V4_ACC(3);
   }
 #undef V4_STAGE
 #undef V4_SLOT
 #undef V4_DMA
-#ifdef VIT_GEMM_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  V4_ACC(7);
-  if (threadIdx.x == 0 && blockIdx.x < 16384) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) vit_stamps[blockIdx.x * 8 + k] = st_acc_[k];
-  }
-#endif
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1611,12 +1471,11 @@ bool aligned(const void* p, int a) { return p == nullptr || (((uintptr_t)p) % a)
 
 // bf16 kernels: 1 = register-staged 128x128, 2 = LDS-DMA 128x128, 4 = LDS-DMA 256x256 ping-pong with LDS-staged
 // epilogue (3 = 4: the former 256-row experiment was removed).
-// VIT_GEMM_IMPL forces a kernel (A/B runs and the per-variant tests); 0 / unset = automatic: v4 when both output
-// dims span a 256 tile, else v2.
+// Option "gemm_impl" forces a kernel (A/B runs and the per-variant tests); 0 = automatic: v4 when both output dims
+// span a 256 tile, else v2.
 int gemm_impl_env() {
-  const char* v = getenv("VIT_GEMM_IMPL");
-  if (v && v[0] >= '1' && v[0] <= '4') return v[0] - '0';
-  return 0;
+  const int64_t v = vit::opt(vit::OPT_GEMM_IMPL);
+  return (v == 1 || v == 2 || v == 4) ? (int)v : 0;
 }
 
 int gemm_impl(int64_t m, int64_t n) {
@@ -1632,14 +1491,13 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
   *m_main = d->m;
   if (d->split_k > 1 || d->in_dtype != VIT_BF16 || d->k % BK != 0 || d->m <= 0 || d->n <= 0) return 1;
   if (gemm_impl(d->m, d->n) != 4 || d->out_group_rows != 0 || d->res_rowmod != 0) return 1;
-  const char* v = getenv("VIT_GEMM_TAIL");
-  if (v && v[0] == '0') return 1;
+  if (!vit::opt(vit::OPT_GEMM_TAIL)) return 1;
   const int64_t tn = (d->n + 255) / 256, tm = (d->m + 255) / 256, nkt = d->k / BK;
   const int64_t rounds = tm * tn / 256;
   // measured (ViT-B/16 B=256, N = 768): a net win at K >= 2304, a loss at K = 768, where a tile's k-loop is short
   // against the slab round trip.  Re-measured with the persistent kernel (tools/bench_ab.sh, whole step): the tail
-  // saves 0.45 ms/step; extending it to K = 768 (VIT_GEMM_TAIL_MINKT=8: proj, fc1, dgrad fc2 / proj) costs 1.0 ms.
-  static const int64_t min_kt = [] { const char* e = getenv("VIT_GEMM_TAIL_MINKT"); return e ? atoll(e) : 32; }();
+  // saves 0.45 ms/step; extending it to K = 768 (gemm_tail_min_kt 8: proj, fc1, dgrad fc2 / proj) costs 1.0 ms.
+  const int64_t min_kt = vit::opt(vit::OPT_GEMM_TAIL_MIN_KT);
   if (rounds < 1 || nkt < min_kt) return 1;
   const int64_t mr = rounds * 256 / tn;                    // tile rows that fill whole rounds
   const int64_t tail = (tm - mr) * tn;                     // tiles of the last, partial round
@@ -1652,16 +1510,6 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
 
 }  // namespace
 
-#ifdef VIT_GEMM_STAMPS
-extern "C" int vit_gemm_debug_stamps(void* dst, int64_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(vit_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-extern "C" int vit_gemm_debug_stamps_reset() {
-  void* p = nullptr;
-  if (hipGetSymbolAddress(&p, HIP_SYMBOL(vit_stamps)) != hipSuccess) return 1;
-  return (int)hipMemset(p, 0, sizeof(unsigned long long) * 16384 * 8);
-}
-#endif
 
 extern "C" int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d) {
   if (!d) return 0;
@@ -1676,8 +1524,8 @@ extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dty
   if (in_dtype == VIT_BF16 && k % BK == 0 && gemm_impl(m, n) == 4) {
     const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
     // slices of >= 4 k-tiles; reductions of fewer than 16 k-tiles (the pruned last block's weight gradients: K = B)
-    // may go down to 1 k-tile per slice (VIT_SPLITK_MINKT overrides the minimum)
-    static const int64_t min_env = [] { const char* e = getenv("VIT_SPLITK_MINKT"); return e ? atoll(e) : 0; }();
+    // may go down to 1 k-tile per slice (option splitk_min_kt overrides the minimum)
+    const int64_t min_env = vit::opt(vit::OPT_SPLITK_MIN_KT);
     const int64_t nkt = k / BK, min_kt = min_env > 0 ? min_env : (nkt >= 16 ? 4 : 1);
     const int64_t s = std::min<int64_t>(std::min<int64_t>(256 / tiles, nkt / min_kt), 64);
     return (int)std::max<int64_t>(1, s);
@@ -1775,8 +1623,8 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
       // Tile order inside an XCD's contiguous range: with many tile columns, row-major order puts ONE A panel and ~32
       // B panels on an XCD at once (little L2 reuse); groups of 8 tile rows, column-major inside a group, give ~8 x 4.
       // Measured (tools/gemm_ab.py): 8192^3 1146 -> 1566 TF/s; neutral on the ViT shapes (<= 12 tile columns).
-      const char* gv = getenv("VIT_GEMM_GROUP");
-      g4.group_m = gv ? atoi(gv) : (g4.tiles_n >= 16 ? 8 : 1);
+      const int64_t gopt = vit::opt(vit::OPT_GEMM_GROUP_M);
+      g4.group_m = gopt > 0 ? gopt : (g4.tiles_n >= 16 ? 8 : 1);
       if (g4.group_m < 1) g4.group_m = 1;
     }
     g4.kt_per_split = (nkt + split - 1) / split;
@@ -1798,8 +1646,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
              e.act == VIT_ACT_NONE && !e.aux && !e.use_drop && d->m < 0x7fffffffLL && d->ldres % 8 == 0 &&
              aligned(d->res, 16))
       kind = EPI_PATCH;
-    const char* dk = getenv("VIT_GEMM_EPI_GENERAL");      // A/B switch: force the general epilogue
-    if (dk && dk[0] == '1' && kind != EPI_SLAB) kind = EPI_GENERAL;
+    if (vit::opt(vit::OPT_GEMM_EPI_GENERAL) && kind != EPI_SLAB) kind = EPI_GENERAL;   // A/B: the general epilogue
     // the v4 epilogue instantiation that runs (fast kinds exist for bf16 output and these operand layouts only)
     int launched = EPI_GENERAL;
     if (kind == EPI_SLAB) launched = EPI_SLAB;
@@ -1810,12 +1657,11 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     else if (out_bf && akc && bkc && kind == EPI_PATCH) launched = EPI_PATCH;
     if (launched != EPI_SLAB && launched != EPI_GENERAL && !e.vec8) launched = EPI_GENERAL;  // wide epilogue needs 8-wide rows
     cs_fused = v4 && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
-    // persistent grid (one workgroup per CU looping over items) for the wide-epilogue kinds; VIT_GEMM_PERSIST=0: one
-    // workgroup per item (A/B switch)
+    // persistent grid (one workgroup per CU looping over items) for the wide-epilogue kinds; option gemm_persist 0:
+    // one workgroup per item (A/B switch)
     {
-      const char* pv = getenv("VIT_GEMM_PERSIST");
       const bool persist = launched != EPI_SLAB && launched != EPI_GENERAL && e.act != VIT_ACT_GELU &&
-                           !(d->flags & VIT_FLAG_SHARED_CUS) && !(pv && pv[0] == '0');
+                           !(d->flags & VIT_FLAG_SHARED_CUS) && vit::opt(vit::OPT_GEMM_PERSIST);
       if (persist && g4.nitems > vit_cu_count()) grid4.x = (unsigned)vit_cu_count();
     }
     e.csum = cs_fused ? d->colsum_part : nullptr;

@@ -3,6 +3,9 @@
 // allows (8-16 B per lane), grid-stride, fixed reduction order (bitwise reproducible).
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
+
+#include <atomic>
 
 #include "vit_common.h"
 
@@ -26,6 +29,43 @@ int check_launch(const char* what) {
 
 extern "C" int vit_abi_version(void) { return VIT_ABI_VERSION; }
 extern "C" const char* vit_last_error(void) { return vit::g_err; }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Launch options (vit_hip.h vit_set_option): names, shipped defaults, current values.
+// ---------------------------------------------------------------------------------------------------------------
+namespace {
+struct OptDef {
+  const char* name;
+  int64_t def;
+};
+constexpr OptDef kOpts[vit::OPT_COUNT] = {
+    {"gemm_impl", 0},        {"gemm_tail", 1},          {"gemm_tail_min_kt", 32}, {"splitk_min_kt", 0},
+    {"gemm_group_m", 0},     {"gemm_epi_general", 0},   {"gemm_persist", 1},      {"attn_fwd_split", 0},
+    {"attn_bwd_split", 0},   {"attn_bwd_grid", 0},      {"ln16", 1},              {"ln_al", 1},
+};
+std::atomic<int64_t> g_opt[vit::OPT_COUNT] = {0, 1, 32, 0, 0, 0, 1, 0, 0, 0, 1, 1};
+
+int opt_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < vit::OPT_COUNT; ++i)
+    if (strcmp(name, kOpts[i].name) == 0) return i;
+  return -1;
+}
+}  // namespace
+
+int64_t vit::opt(vit::Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
+
+extern "C" int vit_set_option(const char* name, int64_t value) {
+  const int i = opt_index(name);
+  VIT_REQUIRE(i >= 0, "vit_set_option: unknown option '%s'", name ? name : "(null)");
+  g_opt[i].store(value, std::memory_order_relaxed);
+  return VIT_OK;
+}
+
+extern "C" int64_t vit_get_option(const char* name) {
+  const int i = opt_index(name);
+  return i >= 0 ? g_opt[i].load(std::memory_order_relaxed) : INT64_MIN;
+}
 
 namespace {
 

@@ -410,8 +410,7 @@ __global__ __launch_bounds__(256) void ln_fwd16_kernel(const bf16_t* __restrict_
 
 // the 16-B forward applies: bf16, cols and every row stride multiples of 8, 16-B aligned base pointers
 static bool ln16_ok(int64_t cols, std::initializer_list<int64_t> lds, std::initializer_list<const void*> ptrs) {
-  static const bool on = [] { const char* e = getenv("VIT_LN16"); return !e || atoi(e) != 0; }();
-  if (!on || cols % 8) return false;
+  if (!vit::opt(vit::OPT_LN16) || cols % 8) return false;
   for (int64_t ld : lds)
     if (ld % 8) return false;
   for (const void* p : ptrs)
@@ -494,9 +493,8 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
   const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   const float scale = 1.0f / (1.0f - drop_p);
   hipStream_t s = VIT_STREAM(stream);
-  // bf16 rows up to 3072 columns: per-wave accumulators in LDS (13 KiB x NV per block); VIT_LN_AL=0: registers
-  const char* al_env = getenv("VIT_LN_AL");
-  const bool al = !(al_env && al_env[0] == '0');
+  // bf16 rows up to 3072 columns: per-wave accumulators in LDS (13 KiB x NV per block); option ln_al 0: registers
+  const bool al = vit::opt(vit::OPT_LN_AL) != 0;
   if (dtype == VIT_BF16) {
 #define CALLB(NV)                                                                                                 \
   if (al && NV <= 12)                                                                                             \
@@ -513,7 +511,7 @@ extern "C" int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, in
   // fp32 (the parity path and the classifier head's LN(4D)): LDS accumulators for the wide rows (NV 6-12), whose
   // register form spilled ~350 VGPRs (the head's LN backward, B x 3072: 133 -> 26.5 us)
 #define CALLF(NV)                                                                                            \
-  if (NV >= 6 && NV <= 12 && !(al_env && al_env[0] == '0'))                                                  \
+  if (NV >= 6 && NV <= 12 && al)                                                  \
     ln_bwd_kernel<float, NV, (NV >= 6 && NV <= 12)><<<(unsigned)parts, 256, 0, s>>>(                         \
         (const float*)dy, lddy, (const float*)x, ldx, gamma, mean, rstd, (const float*)dres, (float*)dx_out, \
         (float*)drop_out, thr, scale, drop_seed, (const uint8_t*)drop_mask, partial, osum != 0, parts, rows, cols); \
