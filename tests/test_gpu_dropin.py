@@ -212,11 +212,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("side_stream", [False, True])
-def test_rccl_bucket_allreduce_world1_bitwise(side_stream):
+@pytest.mark.parametrize("side_stream,comm", [(False, "fp32"), (True, "fp32"), (False, "bf16"), (True, "bf16")])
+def test_rccl_bucket_allreduce_world1_bitwise(side_stream, comm):
     """The engine's RCCL branch (ReduceOp.AVG on the `nccl` backend = RCCL, launched per block bucket inside the
     backward, optionally from the weight-gradient side stream) on a one-rank group: gradients equal the
-    non-parallel run bit for bit."""
+    non-parallel run bit for bit; with bf16 buckets (enable_data_parallel(grad_dtype=torch.bfloat16)) they equal the
+    non-parallel gradients rounded to bf16 (the average of one rank), and comm_exposed_ms() reports a time."""
     import torch.distributed as dist
     ocfg = _hd64_cfg(batch=4)
     st = O.init_state(ocfg, seed=8)
@@ -227,11 +228,15 @@ def test_rccl_bucket_allreduce_world1_bitwise(side_stream):
         m = _model(ocfg, st, torch.bfloat16).train()
         m.hip_engine.concurrent_wgrad = side_stream
         if ddp:
-            m.enable_data_parallel(force=True)
+            m.enable_data_parallel(force=True, grad_dtype=torch.bfloat16 if comm == "bf16" else torch.float32)
             assert m.hip_engine.ddp_enabled and dist.get_backend() == "nccl"
+            m.hip_engine.time_comm = True
         torch.manual_seed(3)
         cross_entropy(m(x), y).backward()
         torch.cuda.synchronize()
+        if ddp:
+            t = m.hip_engine.comm_exposed_ms()
+            assert t is not None and t >= 0.0
         return m.hip_engine.G.clone()
 
     g_plain = grads(False)
@@ -241,7 +246,7 @@ def test_rccl_bucket_allreduce_world1_bitwise(side_stream):
         g_ddp = grads(True)
     finally:
         dist.destroy_process_group()
-    assert torch.equal(g_plain, g_ddp)
+    assert torch.equal(g_plain.bfloat16().float() if comm == "bf16" else g_plain, g_ddp)
 
 
 def test_frozen_parameters_and_input_gradient():
