@@ -129,7 +129,17 @@ def host_topology():
                     phys = core = None
     except OSError:
         pass
-    return {"affinity_cpus": affinity, "omp_num_threads": share or None, "host_logical_cpus": os.cpu_count(),
+    quota = None                                   # cgroup v2 CPU bandwidth limit (e.g. "1600000 100000" = 16 CPUs)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"affinity_cpus": affinity, "cgroup_cpu_quota": quota, "usable_cpus": usable,
+            "omp_num_threads": share or None, "host_logical_cpus": os.cpu_count(),
             "sockets": len(sockets) or None, "physical_cores": len(cores) or None}
 
 
@@ -162,17 +172,21 @@ def _cpu_leg(img, nc, threads, budget_s):
 
 def cpu_baseline(img, nc, budget_s=20.0):
     """The repo's own CPU training step (train.py time_steps -> VisionTransformer/_cpu.py, torch.optim.AdamW) on every
-    CPU in this process's affinity mask (the value), and again on the box's OMP_NUM_THREADS share when that is
-    smaller (`share`)."""
+    CPU this process can use: its affinity mask, capped by the cgroup CPU quota when one is set (the GPU box shows
+    256 affinity CPUs but grants a 16-CPU quota; 256 threads on 16 CPUs time-slice each other to a standstill).  Also
+    on the box's OMP_NUM_THREADS share when that is smaller (`share`)."""
     topo = host_topology()
-    full = _cpu_leg(img, nc, topo["affinity_cpus"], budget_s)
+    n = topo["usable_cpus"]
+    full = _cpu_leg(img, nc, n, budget_s)
+    why = "every CPU of the affinity mask" if n == topo["affinity_cpus"] else \
+        f"the cgroup CPU quota ({n} of {topo['affinity_cpus']} affinity CPUs)"
     out = {"value": full["images_per_s"], "unit": "images/s", "cores": full["threads"], "kind": "port",
            "sample": f"repo train.py host step (VisionTransformer/_cpu.py fwd+CE+bwd + torch AdamW, dropout on), "
                      f"ViT-Base/16 {img}^2 fp32 B32, 1 warmup + {full['steps']} timed steps, "
-                     f"{full['threads']} threads (every CPU of the affinity mask)",
+                     f"{full['threads']} threads ({why})",
            "topology": topo, "c1": full["c1"]}
     share = topo["omp_num_threads"]
-    if share and share < topo["affinity_cpus"]:
+    if share and share < n:
         sh = _cpu_leg(img, nc, share, budget_s)
         out["share"] = {"threads": share, "images_per_s": sh["images_per_s"], "c1": sh["c1"],
                         "note": "the GPU box's OMP_NUM_THREADS share per GPU"}

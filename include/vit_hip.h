@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 9
+#define VIT_ABI_VERSION 10
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -168,14 +168,18 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, 
  *   lse[B][H][T] (natural log of the row softmax denominator, scaled-logit domain) saved for backward;
  *   probs [B][H][T][T] f32 optional (the `.attention_probs` side attribute, transformer.py:48).
  * bf16 & hd == 64: flash-style MFMA kernels (K/V tiles in LDS, online softmax); otherwise a generic VALU kernel.
- * o32 (bf16 only, optional): the forward also stores O unrounded, [B*T][D] f32, and the backward takes it to form
- *   delta = rowsum(dO * O) exactly in fp32.  Under the reference's x sqrt(hd) logit scale most softmax rows saturate,
- *   dS = P (dP - delta) becomes a small difference, and delta from the bf16 O dominates the Q / K gradients; with
- *   o32 == NULL the backward uses the bf16 O (standard flash-attention practice, cheaper).
+ * Under the reference's x sqrt(hd) logit scale most softmax rows saturate and dS = P (dP - delta) becomes a small
+ *   difference, so delta = rowsum(dO * O) must be exact to fp32 rounding:
+ *   - the fused backward (bf16, hd == 64, T <= 256: every ViT-B/L 224^2 config) forms delta = rowsum(P * dP) itself
+ *     from the fp32 P and dP it computes anyway; it reads neither `o` nor `o32`;
+ *   - the tiled backward (T > 256) takes delta from o32 when given: the forward then also stores O unrounded,
+ *     [B*T][D] f32 (o32 == NULL: the bf16 O, standard flash-attention practice, cheaper but inexact).
+ *   vit_attn_bwd_uses_o32() says which one a shape runs (1: pass o32 to the forward and the backward).
  * bwd: dqkv[B*T][3*D]; workspace = vit_attn_bwd_workspace_bytes.
  * ------------------------------------------------------------------------------------------------------------ */
 int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, float* probs, int64_t B, int64_t T, int64_t H,
                  int64_t hd, float scale, int32_t dtype, void* stream);
+int vit_attn_bwd_uses_o32(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
 int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
 int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d_o, const float* lse, void* dqkv,
                  int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype, void* workspace,

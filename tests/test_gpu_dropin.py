@@ -145,11 +145,13 @@ def test_eval_forward_and_attention_probs_vs_oracle(dtype):
 
 
 @pytest.mark.parametrize("T", [197, 577])
-def test_attention_backward_exact_delta_under_saturation(T):
+def test_attention_backward_exact_delta_under_saturation(libopt, T):
     """The x sqrt(hd) scale saturates most softmax rows (max P > 0.99); there dS = P (dP - delta) is a tiny difference.
-    With the forward's fp32 O (o32) the backward's delta is exact to fp32 and dQ / dK track an fp64 evaluation on the
-    same bf16 Q, K, V as closely as rounding dS to bf16 allows (emulated: ~2e-3); delta from the bf16 O does not.
-    Gradient only on query 0 of each image (the last block of the model: the classifier reads token 0)."""
+    The shipped backward forms delta exactly to fp32 — T <= 256: the fused kernel from its own fp32 P and dP (no O
+    read at all); T > 256: the tiled kernels from the forward's fp32 O (o32) — and dQ / dK track an fp64 evaluation on
+    the same bf16 Q, K, V as closely as rounding dS to bf16 allows (emulated: ~2e-3); delta from the bf16 O (the tiled
+    kernels without o32) does not.  Gradient only on query 0 of each image (the last block of the model: the
+    classifier reads token 0)."""
     B, H, hd = 4, 12, 64
     D = H * hd
     g = torch.Generator().manual_seed(31)
@@ -161,11 +163,14 @@ def test_attention_backward_exact_delta_under_saturation(T):
     d_o = d_o.view(B * T, D).to(torch.bfloat16)
     scale = hd ** 0.5
     qd, dd = qkv.to(DEV), d_o.to(DEV)
-    o32 = torch.empty(B * T, D, dtype=torch.float32, device=DEV)
+    uses_o32 = _ops.attn_bwd_uses_o32(B, T, H, hd, torch.bfloat16)
+    assert uses_o32 == (T > 256)
+    o32 = torch.empty(B * T, D, dtype=torch.float32, device=DEV) if uses_o32 else None
     o, lse = _ops.attn_fwd(qd, B, T, H, hd, scale, o32=o32)
     o_ref, lse_ref = _ops.attn_fwd(qd, B, T, H, hd, scale)
     assert torch.equal(o, o_ref) and torch.equal(lse, lse_ref)
     exact = _ops.attn_bwd(qd, o, dd, lse, B, T, H, hd, scale, o32=o32).double().cpu()
+    libopt("attn_bwd_split", 1)                        # the tiled kernels with delta from the bf16 O
     approx = _ops.attn_bwd(qd, o, dd, lse, B, T, H, hd, scale).double().cpu()
     # fp64 reference on the same bf16 inputs
     q, k, v = (qkv.double().view(B, T, 3, H, hd)[:, :, i].transpose(1, 2) for i in range(3))

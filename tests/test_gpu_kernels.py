@@ -448,19 +448,20 @@ def test_attention_bwd_fused_matches_split(libopt, T):
     assert (fused.float() - split.float()).abs().max().item() <= 2e-2 * max(1.0, g.abs().max().item())
 
 
-@pytest.mark.parametrize("o32", [False, True])
-def test_attention_bwd_shared_cus_bitwise(o32):
-    """VIT_FLAG_SHARED_CUS (one workgroup per (image, head) instead of the persistent one-per-CU grid that stages the
-    next item during the current one): bitwise the same dQ / dK / dV, with more items than CUs."""
+@pytest.mark.parametrize("grid", [0, 7, 100])
+def test_attention_bwd_shared_cus_bitwise(libopt, grid):
+    """VIT_FLAG_SHARED_CUS (one workgroup per (image, head) instead of the persistent grid that stages the next item
+    during the current one) and persistent grids of other sizes (attn_bwd_grid; 0 = one per CU): bitwise the same
+    dQ / dK / dV, with more items than workgroups (the in-kernel delta is a fixed-order sum)."""
     torch.manual_seed(3)
     B, H, hd, T = 24, 12, 64, 197                       # 288 items
     D = H * hd
     qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).bfloat16()
-    o32_t = torch.empty(B * T, D, device=DEV) if o32 else None
-    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0, o32=o32_t)
+    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
     d_o = torch.randn(B * T, D, device=DEV).bfloat16()
-    a = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, o32=o32_t)
-    b = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, o32=o32_t, shared_cus=True)
+    b = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, shared_cus=True)    # one workgroup per item
+    libopt("attn_bwd_grid", grid)
+    a = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0)
     assert torch.equal(a, b)
 
 

@@ -1,5 +1,6 @@
-"""Time the attention kernels at the ViT-B/16 training shape (B=256, T=197, H=12, hd=64, bf16).
-    python tools/attn_bench.py [--reps 20]"""
+"""Time the attention kernels at the ViT-B/16 training shape (B=256, T=197, H=12, hd=64, bf16) and check the
+backward against an fp64 torch evaluation on the same bf16 inputs (a few images).
+    python tools/attn_bench.py [--reps 20] [--T 577]"""
 import argparse
 import os
 import sys
@@ -7,7 +8,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vision-transformer_amd"))
 import torch  # noqa: E402
-from VisionTransformer import _ops  # noqa: E402
+from VisionTransformer import _lib, _ops  # noqa: E402
 
 
 def timeit(fn, reps):
@@ -23,34 +24,57 @@ def timeit(fn, reps):
     return sorted(ts)[len(ts) // 2]
 
 
+def ref_grads(qkv, d_o, B, T, H, hd, scale, nb):
+    """fp64 dQ/dK/dV of images 0..nb-1 (torch autograd on the bf16 values)."""
+    D = H * hd
+    x = qkv[:nb * T].double().view(nb, T, 3, H, hd).permute(2, 0, 3, 1, 4).detach().requires_grad_(True)
+    q, k, v = x[0], x[1], x[2]
+    p = torch.softmax(q @ k.transpose(-1, -2) * scale, dim=-1)
+    o = p @ v
+    g = d_o[:nb * T].double().view(nb, T, H, hd).permute(0, 2, 1, 3)
+    (o * g).sum().backward()
+    return x.grad.permute(1, 3, 0, 2, 4).reshape(nb * T, 3 * D)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--T", type=int, default=197, help="tokens (577 = 384^2 / patch 16 + cls: the tiled kernels)")
+    ap.add_argument("--H", type=int, default=12)
     args = ap.parse_args()
-    B, T, H, hd = args.batch, args.T, 12, 64
+    B, T, H, hd = args.batch, args.T, args.H, 64
     D = H * hd
+    scale = 8.0
     torch.manual_seed(0)
     qkv = (torch.randn(B * T, 3 * D, device="cuda") * 0.5).bfloat16()
-    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
+    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, scale)
     d_o = torch.randn(B * T, D, device="cuda").bfloat16()
     fl_f = 4.0 * B * H * T * T * hd
     fl_b = 10.0 * B * H * T * T * hd
-    t = timeit(lambda: _ops.attn_fwd(qkv, B, T, H, hd, 8.0), args.reps)
-    print(f"attn fwd          {t:8.1f} us  {fl_f / t / 1e6:7.1f} TF (4 T^2 hd per head)")
-    t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0), args.reps)
-    print(f"attn bwd fused    {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF (10 T^2 hd per head)")
-    # the training configuration: the forward also stores O in fp32, the backward forms delta from it (attn_delta)
-    o32 = torch.empty(B * T, D, device="cuda")
-    t = timeit(lambda: _ops.attn_fwd(qkv, B, T, H, hd, 8.0, o32=o32), args.reps)
-    print(f"attn fwd +o32     {t:8.1f} us  {fl_f / t / 1e6:7.1f} TF")
-    t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0, o32=o32), args.reps)
-    print(f"attn bwd +delta   {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF (attn_delta from o32 + fused)")
-    os.environ["VIT_ATTN_BWD_SPLIT"] = "1"
-    t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, 8.0), args.reps)
-    print(f"attn bwd split    {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF")
-    os.environ.pop("VIT_ATTN_BWD_SPLIT")
+    uses_o32 = _ops.attn_bwd_uses_o32(B, T, H, hd, torch.bfloat16)
+    o32 = torch.empty(B * T, D, device="cuda") if uses_o32 else None
+    t = timeit(lambda: _ops.attn_fwd(qkv, B, T, H, hd, scale, o32=o32), args.reps)
+    print(f"attn fwd (training form{', +o32' if uses_o32 else ''})  {t:8.1f} us  {fl_f / t / 1e6:7.1f} TF "
+          f"(4 T^2 hd per head)")
+    ws = torch.empty(_ops.attn_bwd_workspace_bytes(B, T, H, hd, torch.bfloat16) // 4 + 1, device="cuda")
+    dq = torch.empty_like(qkv)
+    t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=dq, workspace=ws, o32=o32), args.reps)
+    print(f"attn bwd ({'tiled + attn_delta' if uses_o32 else 'fused, in-kernel delta'})  {t:8.1f} us  "
+          f"{fl_b / t / 1e6:7.1f} TF (10 T^2 hd per head)")
+    nb = 4
+    ref = ref_grads(qkv, d_o, B, T, H, hd, scale, nb)
+    got = dq[:nb * T].double()
+    for name, sl in (("dQ", slice(0, D)), ("dK", slice(D, 2 * D)), ("dV", slice(2 * D, 3 * D))):
+        err = float((got[:, sl] - ref[:, sl]).norm() / ref[:, sl].norm())
+        print(f"  {name} rel err vs fp64 (images 0..{nb - 1}): {err:.2e}")
+    if not uses_o32:
+        with _lib.option("attn_bwd_split", 1):
+            o32s = torch.empty(B * T, D, device="cuda")
+            _ops.attn_fwd(qkv, B, T, H, hd, scale, o32=o32s)
+            t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=dq, workspace=ws, o32=o32s),
+                       args.reps)
+            print(f"attn bwd tiled (attn_delta from o32 + dkdv + dq)  {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF")
 
 
 if __name__ == "__main__":

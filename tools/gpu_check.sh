@@ -21,6 +21,8 @@ for s in $STEPS; do
           --shapes ${AB_SHAPES:-fwd_fc1,fwd_fc1m,dgrad_fc2,dgrad_fc2m} > "$OUT/ab.log" 2>&1 ;;
     model) timeout -k 10 900 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_dropin.py -x -v -m gpu \
              -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/model.log" 2>&1 ;;
+    attn) timeout -k 10 300 python -u tools/attn_bench.py > "$OUT/attn.log" 2>&1 &&
+          timeout -k 10 300 python -u tools/attn_bench.py --T 577 --batch 64 >> "$OUT/attn.log" 2>&1 ;;
     ln) timeout -k 10 300 python -u tools/ln_bench.py > "$OUT/ln.log" 2>&1 ;;
     lnab) for v in ${LN_VARIANTS:-}; do
             VIT_HIP_LIB=tools/variants/libvit_hip_$v.so timeout -k 10 120 python -u tools/ln_bench.py > "$OUT/ln_$v.log" 2>&1 || break

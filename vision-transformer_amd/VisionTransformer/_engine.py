@@ -438,8 +438,10 @@ class Engine:
             probs = None
             if want_probs:
                 probs = torch.empty(B, H, T, T, dtype=torch.float32, device=x.device)
-            # training forward in bf16: also keep O unrounded for the backward's exact delta (see vit_hip.h)
-            o32 = torch.empty(M, D, dtype=torch.float32, device=x.device) if (save and dt != torch.float32) else None
+            # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta; the
+            # fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
+            o32 = (torch.empty(M, D, dtype=torch.float32, device=x.device)
+                   if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
             mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                          else 0))
             o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
@@ -668,8 +670,9 @@ class Engine:
                 dxm_full = torch.zeros(M, D, dtype=dt, device=dev)
                 _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
                 do, dx_mid = do_full, dxm_full
-            mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 8 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
-                                                                                          else 0))
+            # bytes: qkv, dO, dqkv (+ O and o32 for the tiled backward's delta pass)
+            mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 7 * M * D * es + 4 * B * H * T + (M * D * es + 4 * M * D if o32
+                                                                                          is not None else 0))
             dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
                                  workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32,
                                  shared_cus=self.shared_cus)

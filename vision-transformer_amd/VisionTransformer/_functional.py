@@ -171,7 +171,8 @@ class HeadAttentionFn(torch.autograd.Function):
             _ops.copy2d(w.contiguous(), D, wpack[i * hd:(i + 1) * hd], D, hd, D)
         qkv = _ops.linear(x2, wpack)
         probs = torch.empty(B, 1, T, T, dtype=torch.float32, device=x.device)
-        o32 = torch.empty(B * T, hd, dtype=torch.float32, device=x.device) if dt == torch.bfloat16 else None
+        o32 = (torch.empty(B * T, hd, dtype=torch.float32, device=x.device)
+               if _ops.attn_bwd_uses_o32(B, T, 1, hd, dt) else None)
         o, lse = _ops.attn_fwd(qkv, B, T, 1, hd, float(hd) ** 0.5, probs=probs, o32=o32)
         ctx.save_for_backward(x2, wpack, qkv, o, lse, o32)
         ctx.dims = (B, T, D, hd)

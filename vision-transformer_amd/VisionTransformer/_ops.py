@@ -169,7 +169,8 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, dr
 
 
 def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, o32=None, stream=None):
-    """o = softmax(scale Q K^T) V per head; `o32` (bf16 only): also store O unrounded (fp32) for attn_bwd's delta."""
+    """o = softmax(scale Q K^T) V per head; `o32` (bf16 only): also store O unrounded (fp32) for attn_bwd's delta
+    where attn_bwd_uses_o32() says the backward takes it."""
     _need_cuda(qkv)
     D = H * hd
     o = torch.empty(B * T, D, dtype=qkv.dtype, device=qkv.device) if o is None else o
@@ -177,6 +178,12 @@ def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, o32=None, st
     _lib.call("vit_attn_fwd", _ptr(qkv), _ptr(o), _ptr(o32), _ptr(lse), _ptr(probs), B, T, H, hd, scale,
               dtype_code(qkv), _stream(stream))
     return o, lse
+
+
+def attn_bwd_uses_o32(B, T, H, hd, dtype):
+    """True when attn_bwd at this shape forms delta from the forward's fp32 O (the tiled T > 256 path); the fused
+    T <= 256 backward forms it from P and dP itself and reads neither O nor o32."""
+    return bool(_lib.load().vit_attn_bwd_uses_o32(B, T, H, hd, dtype_code(dtype)))
 
 
 def attn_bwd_workspace_bytes(B, T, H, hd, dtype):

@@ -222,12 +222,15 @@ VIT_DEV bf16x8_t glb_frag(const bf16_t* __restrict__ src, int64_t ld, int64_t ro
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// 8 consecutive accumulator registers (8s2 .. 8s2+7) -> bf16 B fragment
+// 8 consecutive accumulator registers (8s2 .. 8s2+7) -> bf16 B fragment (v_cvt_pk_bf16_f32 pairs: RNE, as f2bf)
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+typedef float f32x2_v __attribute__((ext_vector_type(2)));
 VIT_DEV bf16x8_t pack8(const float* x) {
-  s16x8 v;
+  uint32_t w[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(x[j]);
-  return __builtin_bit_cast(bf16x8_t, v);
+  for (int q = 0; q < 4; ++q)
+    w[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_v{x[2 * q], x[2 * q + 1]}, bf16x2_v));
+  return __builtin_bit_cast(bf16x8_t, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
 VIT_DEV f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
@@ -566,14 +569,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 
 // ---------------------------------------------------------------------------------------------------------------
 // Fused backward for T <= 256 (ViT: T = 197): one 8-wave workgroup per (image, head), everything from LDS.
-//   LDS: K, Q, dO as [Tp][64] images (Tp = T rounded up to 32, rows >= T zero), lse2 / delta per query, and a
-//   double-buffered dS^T image [Tp keys][32 queries].  delta = rowsum(dO * O) is computed here (no separate pass).
+//   LDS: K, Q, dO (and V when it fits) as [Tp][64] images (Tp = T rounded up to 32), lse2 per query, the delta
+//   partials, a double-buffered dS^T image [Tp keys][32 queries] and a double-buffered dQ staging block.
 //   Wave w owns key block w (32 keys: its K / V fragments live in registers, dK / dV accumulate in registers) and
-//   walks the query blocks qb:  S^T, dP^T (keys on lanes) -> P, dS -> dV += dO^T P, dK += Q^T dS, dS^T -> LDS;
-//   barrier; then dQ[qb] (32 x 64) is split over the 8 waves as 16x16 tiles (16x16x32 MFMA over all Tp keys):
-//   no recomputation of P, no atomics, no cross-wave reduction — deterministic.
+//   walks the query blocks qb:  S, dP (keys on lanes) -> P -> dV += dO^T P, delta = rowsum(P * dP) over the key
+//   waves, dS = P (dP - delta) -> dK += Q^T dS, dS^T -> LDS; then dQ[qb] (32 x 64) is split over the 8 waves as
+//   16x16 tiles (16x16x32 MFMA over all Tp keys): no recomputation of P, no atomics — deterministic.
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int FB_TMAX = 256;
+#ifndef ATT_DWAV
+#define ATT_DWAV 1
+#endif
+#ifndef ATT_KVLDS
+#define ATT_KVLDS 1
+#endif
 
 VIT_DEV __amdgpu_buffer_rsrc_t make_rsrc_b(const void* base, int64_t bytes) {
   const uint32_t nrec = bytes >= 0x7fffffffLL ? 0x7fffffffu : (uint32_t)bytes;
@@ -609,14 +618,15 @@ VIT_DEV void dma_head_slice(__amdgpu_buffer_rsrc_t rs, int64_t row0, int64_t ld,
   }
 }
 
-// Row-contiguous store of a [rows][64] bf16 LDS image (plain [r][64], no swizzle) to global rows (row stride ld):
-// 8 lanes per 128-B row.
+// Row-contiguous store of a [rows][64] bf16 LDS image (row stride RS elements, no swizzle) to global rows (row stride
+// ld): 8 lanes per 128-B row.
+template <int RS>
 VIT_DEV void store_rows64(const bf16_t* img, int rows, int valid_rows, bf16_t* dst, int64_t ld, int tid,
                           int nthreads) {
   for (int q = tid; q < rows * 8; q += nthreads) {
     const int r = q >> 3, c = q & 7;
     if (r < valid_rows)
-      *reinterpret_cast<uint4*>(dst + (int64_t)r * ld + c * 8) = *reinterpret_cast<const uint4*>(img + r * 64 + c * 8);
+      *reinterpret_cast<uint4*>(dst + (int64_t)r * ld + c * 8) = *reinterpret_cast<const uint4*>(img + r * RS + c * 8);
   }
 }
 
@@ -648,33 +658,85 @@ VIT_DEV void dma_slice_g(const bf16_t* base, int64_t row0, int64_t ld, int64_t c
   for (int pc = wave; pc < Tp / 8; pc += 8) dma_piece(base, row0, ld, col0, Tn, img, pc, lane);
 }
 
+// Row sums of a 32x32 accumulator tile over its 32 columns (the keys, on the lanes of each half-wave): t[r] holds
+// element (row acc_row(r, hf), column lane & 31).  One v_permlane16_swap per register pair folds the two 16-lane rows
+// of a half-wave (even rows keep registers 0-7, odd rows 8-15), then four DPP steps (xor 8, 7, 2, 1 inside a row)
+// finish the sums.  Every lane of 16-lane row R ends with the sums of registers 8 (R & 1) + j, j = 0..7.  The pairing
+// is fixed, so the result does not depend on timing (deterministic).
+VIT_DEV void rowsum32(const float (&t)[16], float (&u)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(t[j]), __float_as_uint(t[j + 8]), false, false);
+    u[j] = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+  }
+  // v_add_f32 with a DPP source, 8 independent registers per step (hipcc does not fold v_mov_dpp into the add here);
+  // a DPP read needs 2 wait states after the VALU write of its register: the s_nop covers the first step, later
+  // steps read registers written 8 instructions earlier
+#define VIT_DPP_ADD8(CTRL)                                                                                        \
+  asm volatile("s_nop 1\n\t"                                                                                    \
+               "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %4, %4, %4 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %5, %5, %5 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %6, %6, %6 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
+               "v_add_f32_dpp %7, %7, %7 " CTRL " row_mask:0xf bank_mask:0xf"                                   \
+               : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]))
+  VIT_DPP_ADD8("row_ror:8");
+  VIT_DPP_ADD8("row_half_mirror");
+  VIT_DPP_ADD8("quad_perm:[2,3,0,1]");
+  VIT_DPP_ADD8("quad_perm:[1,0,3,2]");
+#undef VIT_DPP_ADD8
+}
+
 // Persistent: workgroup g handles items (image, head) g, g + gridDim.x, ...  The next item's operands are staged while
-// this one computes: its Q / dO 32-row blocks are LDS-DMA'd into this item's blocks as they die (block qb is last read
-// by pair(qb)), its K and O (only needed for delta; into the dS^T region) right after the last dQ block, its lse into a
-// register.  The first item's staging is exposed, later ones only the K / O tail behind the dK / dV stores.  gridDim.x == items gives one item per
-// workgroup (no prefetch).  dK / dV leave registers directly (the Q / dO images already hold the next item).
+// this one computes: its dO / Q 32-row blocks are LDS-DMA'd into this item's blocks as they die (dO block qb after
+// front(qb), Q block qb after back(qb)), its V after the first barrier, its K right after the last dQ block, its lse
+// into a register.  gridDim.x == items gives one item per workgroup (no prefetch).  dK / dV leave registers directly.
+//
+// delta[q] = sum_k P[q][k] dP[q][k] (= rowsum(dO * O) in exact arithmetic) is formed here from the fp32 P and dP the
+// backward computes anyway, so neither O nor an fp32 copy of it is read: under the reference's x sqrt(hd) logit scale
+// most softmax rows saturate and dS = P (dP - delta) is a small difference, which a delta from the bf16-rounded O
+// would swamp; this one is consistent with the kernel's own P to fp32 rounding.  A query block qb runs in two halves
+// one barrier apart, software-pipelined with the neighbouring blocks (iteration it = one barrier interval):
+//   front(it):   S, dP (keys on lanes) -> P; dV += dO^T P; each key wave's partial rowsum(P * dP) -> LDS
+//   back(it-1):  delta = the key waves' partials in wave order; dS = P (dP - delta); dK += Q^T dS; dS^T -> LDS
+//   dq(it-2):    dQ block = dS K over all keys, split over the 8 waves as 16x16 tiles -> LDS staging
+//   store(it-3): the staged dQ block -> global, full rows
+// P and dP of the block in flight stay in registers across the barrier.  No atomics, no cross-wave reduction of
+// results beyond the fixed-order delta sum: deterministic.
 template <int NQB>
-__global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
-                                                         const bf16_t* __restrict__ d_o, const float* __restrict__ lse,
-                                                         const float* __restrict__ delta_in, bf16_t* __restrict__ dqkv,
+__global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ d_o,
+                                                         const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
                                                          int64_t Tn64, int64_t H, int64_t items, float scale) {
   constexpr int Tp = NQB * 32;                        // T rounded up to 32 (compile time: the dQ sum unrolls)
   constexpr int nqb = NQB;
   constexpr int IMG = Tp * HD;                        // elements per [Tp][64] image
-  constexpr int DST = Tp * 32;                        // elements per dS^T image [Tp][32]
-  constexpr int QST = 32 * HD;                        // dQ block staging [32][64]
+  // dS^T image [Tp keys][32 queries]: the 8-B unit u (4 queries) of key row r sits at unit u ^ ((r >> 1) & 7), which
+  // makes both its ds_write_b64 (16 consecutive keys per lane group) and the dQ B-operand ds_read_b64_tr_b16 (8 rows x
+  // 4 units per 32-lane group) bank-conflict free (the plain layout cost 28 extra LDS cycles per store instruction:
+  // 8 keys on one bank pair).  dQ staging rows are padded to 68 elements (136 B: 17 8-B units, odd) so its 16-row
+  // ds_write_b64 groups spread over all banks (a 128-B row put all 16 on one bank pair, 60 extra cycles per store).
+  constexpr int DST = Tp * 32;                        // elements per dS^T image
+  constexpr int QRS = HD + 4;                         // dQ staging row stride (elements)
+  constexpr int QST = 32 * QRS;                       // dQ block staging [32][68]
+  constexpr int NF = Tp + 2 * 8 * 32 + 8 * 32;        // floats: lse2 [Tp], delta partials [2][8][32], per-wave delta [8][32]
+  constexpr int XS = NQB < 8 ? 32 * 32 : 0;           // dS^T scratch of the wave without a key block
   // V image too when it fits in the 160 KiB (Tp <= 224): staged during the previous item instead of read from global
   // at the top of each item (an exposed load round trip per item)
-  constexpr bool VLDS = (4 * IMG + 2 * DST + 2 * QST + 2 * Tp * 2) * 2 <= 160 * 1024;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(VLDS ? 4 : 3) * IMG + 2 * DST + 2 * QST + 2 * Tp * 2];
+  constexpr bool VLDS = (4 * IMG + 2 * DST + 2 * QST + XS) * 2 + NF * 4 <= 160 * 1024;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(VLDS ? 4 : 3) * IMG + 2 * DST + 2 * QST + XS + 2 * NF];
   bf16_t* Ks = smem;
   bf16_t* Qs = Ks + IMG;
   bf16_t* Gs = Qs + IMG;
   bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]
   bf16_t* dQs = dSt + 2 * DST;                         // [2][32][64]
   bf16_t* Vs = dQs + 2 * QST;                          // [Tp][64] when VLDS
-  float* lse2s = reinterpret_cast<float*>(Vs + (VLDS ? IMG : 0));
-  float* dlts = lse2s + Tp;
+  bf16_t* dSx = Vs + (VLDS ? IMG : 0);                 // [32][32] when NQB < 8
+  float* lse2s = reinterpret_cast<float*>(dSx + XS);
+  float* dpart = lse2s + Tp;                           // [2][8][32]
+  float* dwav = dpart + 2 * 8 * 32;                    // [8][32]
 
   const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -682,11 +744,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   const int64_t D = H * HD, ld = 3 * D;
   const float c2 = scale * LOG2E;
 
-  const bool kact = wave < nqb;                       // this wave owns key block `wave`
-  const int kb = wave * 32;
+  // Wave w owns key block w.  A wave without one (w >= nqb: wave 7 at T = 197) runs the same instruction stream on
+  // key block 0 with every key masked (P = 0, so dS = 0 and its dK / dV are never stored): no wave-dependent branch
+  // splits the loop body, which the compiler can then schedule as one block.
+  const bool kact = wave < nqb;
+  const int kb = kact ? wave * 32 : 0;
   const int key = kb + (lane & 31);
-  const bool kmask = kb + 32 > Tn;                    // wave-uniform: this key block has keys >= T
-  const float kbias = key < Tn ? 0.f : -INFINITY;
+  const float kbias = kact && key < Tn ? 0.f : -INFINITY;
   const int dd = wave >> 1, qh = wave & 1;            // this wave's dQ tile: d 16dd.., queries 16qh..
   // Per-lane LDS offsets (elements) inside a 32-row block: the row swizzle aswz(r) only uses bits 1..3 of r, so a
   // block starting at a multiple of 16 rows adds rb * 64 and nothing else.
@@ -715,8 +779,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     const int colk = dd * 16 + 4 * pp, cols = qh * 16 + 4 * pp;
     cf_k[0] = ra * HD + (((colk >> 3) ^ aswz(ra)) << 3) + (colk & 7);
     cf_k[1] = rb2 * HD + (((colk >> 3) ^ aswz(rb2)) << 3) + (colk & 7);
-    cf_s[0] = ra * 32 + cols;
-    cf_s[1] = rb2 * 32 + cols;
+    cf_s[0] = ra * 32 + (((cols >> 2) ^ ((ra >> 1) & 7)) << 2);        // (kc a multiple of 32: same swizzle)
+    cf_s[1] = rb2 * 32 + (((cols >> 2) ^ ((rb2 >> 1) & 7)) << 2);
   }
   auto trd = [&](const bf16_t* base, int o1, int o2) {
     s16x4 lo = tr_read(base + o1);
@@ -728,14 +792,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(base + o));
   };
 
-  // lse (and delta, when precomputed from the fp32 O) of item `it_` -> registers (tid < Tn <= 256)
-  const bool dglob = delta_in != nullptr;
-  float lreg = 0.f, dreg = 0.f;
+  // lse of item `it_` -> a register (tid < Tn <= 256)
+  float lreg = 0.f;
   auto load_lse = [&](int64_t it_) {
-    if (tid < Tn) {
-      lreg = lse[it_ * Tn + tid];
-      if (dglob) dreg = delta_in[it_ * Tn + tid];
-    }
+    if (tid < Tn) lreg = lse[it_ * Tn + tid];
   };
 
   int64_t item = blockIdx.x;
@@ -744,7 +804,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     dma_slice_g(qkv, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane);
     dma_slice_g(qkv, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
     dma_slice_g(d_o, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
-    if (!dglob) dma_slice_g(o, b * Tn, D, h * HD, Tn, Tp, dSt, wave, lane);   // O: only needed for delta
     if (VLDS) dma_slice_g(qkv, b * Tn, ld, 2 * D + h * HD, Tn, Tp, Vs, wave, lane);
     load_lse(item);
   }
@@ -754,129 +813,193 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     const int64_t nxt = item + gridDim.x;
     const bool more = nxt < items;
     const int64_t nb_ = more ? nxt / H : 0, nh_ = more ? nxt % H : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / O DMA, lse
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / V DMA, lse
     if (tid < Tp) lse2s[tid] = tid < Tn ? lreg * LOG2E : INFINITY;
-    if (dglob && tid < Tp) dlts[tid] = tid < Tn ? dreg : 0.f;
     __syncthreads();                                  // every wave's DMA landed
-    // delta[q] = sum_d dO[q][d] O[q][d]: 8 lanes per row (one 16-B chunk each), fixed shuffle-tree order
-    for (int q = tid; q < (dglob ? 0 : Tp * 8); q += 512) {   // Tp * 8 is a multiple of 256: wave-uniform condition
-      {
-        const int r = q >> 3, c = q & 7;
-        const int off = r * HD + ((c ^ aswz(r)) << 3);
-        const s16x8 vg = *reinterpret_cast<const s16x8*>(Gs + off);
-        const s16x8 vo = *reinterpret_cast<const s16x8*>(dSt + off);
-        float sacc = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sacc += bf2f((bf16_t)vo[e]) * bf2f((bf16_t)vg[e]);
-        sacc += __shfl_xor(sacc, 1, 64);
-        sacc += __shfl_xor(sacc, 2, 64);
-        sacc += __shfl_xor(sacc, 4, 64);
-        if (c == 0) dlts[r] = sacc;
-      }
-    }
     bf16x8_t kf[4], vf[4];
-    if (kact) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        kf[s] = row_frag(Ks, kb, s, lane);
+    for (int s = 0; s < 4; ++s) {
+      if (!ATT_KVLDS) kf[s] = row_frag(Ks, kb, s, lane);
+      if (!ATT_KVLDS || !VLDS)
         vf[s] = VLDS ? row_frag(Vs, kb, s, lane) : glb_frag(qkv + b * Tn * ld, ld, kb, Tn, 2 * D + h * HD, s, lane);
-      }
     }
-    lds_barrier();                                    // delta visible
     f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
+    float pc[16], dpc[16];                            // P and dP of the block between front and back
 
-    // pair(qb): this wave's key block against query block qb -> dV, dK accumulate; dS^T block -> dSt[qb & 1]
-    auto pair = [&](int qb) {
+    // front(qb): this wave's key block against query block qb -> P, dV; partial delta -> dpart[qb & 1][wave]
+    auto front = [&](int qb) {
       const int q0 = qb * 32;
       const bf16_t* Qb = Qs + q0 * HD;
       const bf16_t* Gb = Gs + q0 * HD;
       f32x16 sacc = {}, pacc = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        sacc = mfma32(rrd(Qb, rf_off[s]), kf[s], sacc);           // S[q][key]: lane = key
-        pacc = mfma32(rrd(Gb, rf_off[s]), vf[s], pacc);           // dP[q][key]
+#if ATT_KVLDS
+        const bf16x8_t kfs = rrd(Ks + kb * HD, rf_off[s]), vfs = VLDS ? rrd(Vs + kb * HD, rf_off[s]) : vf[s];
+#else
+        const bf16x8_t kfs = kf[s], vfs = vf[s];
+#endif
+        sacc = mfma32(rrd(Qb, rf_off[s]), kfs, sacc);             // S[q][key]: lane = key
+        pacc = mfma32(rrd(Gb, rf_off[s]), vfs, pacc);             // dP[q][key]
       }
-      // registers 4g..4g+3 <-> queries q0 + 8g + 4hf + 0..3: broadcast b128 reads of the statistics
-      float p[16], ds[16];
+      // registers 4g..4g+3 <-> queries q0 + 8g + 4hf + 0..3: broadcast b128 reads of lse2
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2s + q0 + 8 * g + 4 * hf);
-        const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dlts + q0 + 8 * g + 4 * hf);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
-          // queries >= T have lse2 = +inf -> P = 0 exactly
-          p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lv[i]);
-          ds[r] = pacc[r] - dv4[i];
+          // queries >= T have lse2 = +inf, keys >= T kbias = -inf -> P = 0 exactly
+          pc[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lv[i] + kbias);
+          dpc[r] = pacc[r];
         }
       }
-      if (kmask) {                                    // keys >= T (zero K rows) must not contribute
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          p[r] = __builtin_amdgcn_exp2f(sacc[r] * c2 - lse2s[q0 + acc_row(r, hf)] + kbias);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ds[r] *= p[r];
-      const bf16x8_t p0 = pack8(p), p1 = pack8(p + 8), d0 = pack8(ds), d1 = pack8(ds + 8);
+      const bf16x8_t p0 = pack8(pc), p1 = pack8(pc + 8);
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
         dv[db] = mfma32(trd(Gb, tf_off[db][0], tf_off[db][1]), p0, dv[db]);
         dv[db] = mfma32(trd(Gb + 16 * HD, tf_off[db][0], tf_off[db][1]), p1, dv[db]);
-        dk[db] = mfma32(trd(Qb, tf_off[db][0], tf_off[db][1]), d0, dk[db]);
-        dk[db] = mfma32(trd(Qb + 16 * HD, tf_off[db][0], tf_off[db][1]), d1, dk[db]);
       }
-      bf16_t* dS = dSt + (qb & 1) * DST + key * 32 + 4 * hf;
+      float t[16], u[8];
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        float v4[4] = {ds[4 * g4], ds[4 * g4 + 1], ds[4 * g4 + 2], ds[4 * g4 + 3]};
-        st4<bf16_t>(dS + 8 * g4, v4);
+      for (int r = 0; r < 16; ++r) t[r] = pc[r] * dpc[r];
+      rowsum32(t, u);
+      // lane 16R (R = 16-lane row; hf = R >> 1) writes registers 8 (R & 1) + j: queries 16 (R & 1) + 4 hf + 0..3 and
+      // 16 (R & 1) + 8 + 4 hf + 0..3
+      if ((lane & 15) == 0) {
+        float* dp = dpart + (qb & 1) * 256 + wave * 32 + 16 * ((lane >> 4) & 1) + 4 * hf;
+        *reinterpret_cast<f32x4*>(dp) = f32x4{u[0], u[1], u[2], u[3]};
+        *reinterpret_cast<f32x4*>(dp + 8) = f32x4{u[4], u[5], u[6], u[7]};
       }
     };
 
-    // software pipeline: iteration i computes pair(i) (if any) and dQ(i-1) between the same two barriers, and stages
-    // the next item's Q / dO block i-1 (last read by pair(i-1), before the previous barrier)
-    bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
-#pragma unroll 1
-    for (int it = 0; it <= nqb; ++it) {
-      if (it >= 2) {                                  // dQ(it-2) staged in the previous iteration: full-row stores
-        const int qs = (it - 2) * 32;
-        store_rows64(dQs + ((it - 2) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
-      }
-      if (kact && it < nqb) pair(it);
-      if (it >= 1) {
-        const int qb = it - 1;
-        const bf16_t* dS = dSt + (qb & 1) * DST;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // back(qb): delta of query block qb (its partials are behind the last barrier) -> dS -> dK; dS^T -> dSt[qb & 1]
+    auto back = [&](int qb) {
+      const int q0 = qb * 32;
+      const bf16_t* Qb = Qs + q0 * HD;
+      float ds[16];
+#if ATT_DWAV
+      const float* dp = dpart + (qb & 1) * 256 + (lane & 31);
+      float dsum = dp[0];
 #pragma unroll
-        for (int kc = 0; kc < Tp; kc += 32) {
-          const bf16x8_t a = trd(Ks + kc * HD, cf_k[0], cf_k[1]);
-          const bf16x8_t bq = trd(dS + kc * 32, cf_s[0], cf_s[1]);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc, 0, 0, 0);
-        }
-        // D[m = d][n = q]: lane -> q = 16qh + (lane&15), d = 16dd + 4(lane>>4) + i  -> staging [32][64]
-        float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
-        st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * 64 + dd * 16 + 4 * (lane >> 4), v4);
+      for (int w = 1; w < nqb; ++w) dsum += dp[w * 32];  // key-block order: the same sum in every wave
+      float* dw = dwav + wave * 32;
+      dw[lane & 31] = dsum;                           // lanes l and l + 32 store the same value
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 dv4 = *reinterpret_cast<const f32x4*>(dw + 8 * g + 4 * hf);   // this wave's own write above
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ds[4 * g + i] = pc[4 * g + i] * (dpc[4 * g + i] - dv4[i]);
       }
-      if (more && it >= 1) {
-        const int pc = (it - 1) * 4 + (wave & 3);
-        if (wave < 4) dma_piece(qkv, nb_ * Tn, ld, nh_ * HD, Tn, Qs, pc, lane);
-        else dma_piece(d_o, nb_ * Tn, D, nh_ * HD, Tn, Gs, pc, lane);
-        if (it == 1) {
-          load_lse(nxt);                              // after pair(0) consumed the V fragments: no wait on it
-          if (VLDS) dma_slice_g(qkv, nb_ * Tn, ld, 2 * D + nh_ * HD, Tn, Tp, Vs, wave, lane);  // V read at the top
-        }
+#else
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float* dp = dpart + (qb & 1) * 256 + 8 * g + 4 * hf;
+        f32x4 dv4 = *reinterpret_cast<const f32x4*>(dp);
+#pragma unroll
+        for (int w = 1; w < nqb; ++w) dv4 += *reinterpret_cast<const f32x4*>(dp + w * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ds[4 * g + i] = pc[4 * g + i] * (dpc[4 * g + i] - dv4[i]);
       }
-      lds_barrier();                                  // LDS only: the prefetch and the dQ stores stay in flight
+#endif
+      const bf16x8_t d0 = pack8(ds), d1 = pack8(ds + 8);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        dk[db] = mfma32(trd(Qb, tf_off[db][0], tf_off[db][1]), d0, dk[db]);
+        dk[db] = mfma32(trd(Qb + 16 * HD, tf_off[db][0], tf_off[db][1]), d1, dk[db]);
+      }
+      // (a wave without a key block writes its zero dS^T rows to a scratch block instead of key block 0's)
+      bf16_t* dS = (kact ? dSt + (qb & 1) * DST : dSx) + key * 32;
+      const int ksw = (key >> 1) & 7;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {                // queries 8 g4 + 4 hf + 0..3: unit 2 g4 + hf
+        float v4[4] = {ds[4 * g4], ds[4 * g4 + 1], ds[4 * g4 + 2], ds[4 * g4 + 3]};
+        st4<bf16_t>(dS + (((2 * g4 + hf) ^ ksw) << 2), v4);
+      }
+    };
+
+    // dQ(qb) = dS K over all keys: this wave's 16x16 tile of the 32 x 64 block -> staging dQs[qb & 1]
+    auto dq = [&](int qb) {
+      const bf16_t* dS = dSt + (qb & 1) * DST;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < Tp; kc += 32) {
+        const bf16x8_t a = trd(Ks + kc * HD, cf_k[0], cf_k[1]);
+        const bf16x8_t bq = trd(dS + kc * 32, cf_s[0], cf_s[1]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq, acc, 0, 0, 0);
+      }
+      // D[m = d][n = q]: lane -> q = 16qh + (lane&15), d = 16dd + 4(lane>>4) + i  -> staging [32][64]
+      float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
+      st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + (lane & 15)) * QRS + dd * 16 + 4 * (lane >> 4), v4);
+    };
+    bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
+    auto dq_store = [&](int qb) {                     // the staged dQ block -> global, full rows
+      const int qs = qb * 32;
+      store_rows64<QRS>(dQs + (qb & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
+    };
+    // The next item's staging (the last item of a workgroup re-stages itself: the blocks are dead either way, and the
+    // prefetch stays unconditional).  Waves 0-3 take the Q block's 4 pieces, waves 4-7 the dO block's.
+    const int64_t sb_ = more ? nb_ : b, sh_ = more ? nh_ : h;
+    const bool gq = wave < 4;
+    const bf16_t* pf_base = gq ? qkv : d_o;
+    const int64_t pf_ld = gq ? ld : D;
+    bf16_t* pf_img = gq ? Qs : Gs;
+    auto prefetch = [&](int qblk) {                   // Q block qblk (waves 0-3) or dO block qblk + 1 (waves 4-7)
+      dma_piece(pf_base, sb_ * Tn, pf_ld, sh_ * HD, Tn, pf_img, (qblk + (gq ? 0 : 1)) * 4 + (wave & 3), lane);
+    };
+    // iteration it (one barrier interval): store dQ(it-3), back(it-1), front(it), dQ(it-2); the prefetch of dO block
+    // it-1 (dead since front(it-1)) and Q block it-2 (dead since back(it-2)).  Prologue and tail peeled: the steady
+    // iterations 2 .. nqb-1 are branch-free.
+    if constexpr (NQB >= 3) {
+      front(0);
+      lds_barrier();
+      back(0);
+      front(1);
+      if (wave >= 4) prefetch(-1);                    // dO block 0
+      load_lse(more ? nxt : item);                    // after front(0) consumed the V fragments: no wait on it
+      if (VLDS && !ATT_KVLDS) dma_slice_g(qkv, sb_ * Tn, ld, 2 * D + sh_ * HD, Tn, Tp, Vs, wave, lane);  // V: top only
+      lds_barrier();
+      back(1);
+      front(2);
+      dq(0);
+      prefetch(0);                                    // Q block 0, dO block 1
+      lds_barrier();
+#pragma unroll 1
+      for (int it = 3; it < nqb; ++it) {
+        dq_store(it - 3);
+        back(it - 1);
+        front(it);
+        dq(it - 2);
+        prefetch(it - 2);
+        lds_barrier();                                // LDS only: the prefetch and the dQ stores stay in flight
+      }
+      dq_store(nqb - 3);
+      back(nqb - 1);
+      dq(nqb - 2);
+      prefetch(nqb - 2);                              // Q block nqb-2, dO block nqb-1
+      if (VLDS && ATT_KVLDS) dma_slice_g(qkv, sb_ * Tn, ld, 2 * D + sh_ * HD, Tn, Tp, Vs, wave, lane);  // V: fronts done
+      lds_barrier();
+      dq_store(nqb - 2);
+      dq(nqb - 1);
+      if (wave < 4) prefetch(nqb - 1);                // Q block nqb-1
+      lds_barrier();
+      dq_store(nqb - 1);
+    } else {                                          // T <= 64: the same schedule with its conditions
+#pragma unroll 1
+      for (int it = 0; it <= nqb + 1; ++it) {
+        if (it >= 3) dq_store(it - 3);
+        if (it >= 1 && it <= nqb) back(it - 1);
+        if (it < nqb) front(it);
+        if (it >= 2) dq(it - 2);
+        if ((wave >= 4 && it >= 1 && it <= nqb) || (wave < 4 && it >= 2)) prefetch(it - 2);
+        if (it == 1) load_lse(more ? nxt : item);
+        if (VLDS && it == (ATT_KVLDS ? nqb : 1)) dma_slice_g(qkv, sb_ * Tn, ld, 2 * D + sh_ * HD, Tn, Tp, Vs, wave, lane);
+        lds_barrier();
+      }
+      dq_store(nqb - 1);
     }
-    {                                                 // last dQ block
-      const int qs = (nqb - 1) * 32;
-      store_rows64(dQs + ((nqb - 1) & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, 512);
-    }
-    // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K and O
-    if (more) {
-      dma_slice_g(qkv, nb_ * Tn, ld, D + nh_ * HD, Tn, Tp, Ks, wave, lane);
-      if (!dglob) dma_slice_g(o, nb_ * Tn, D, nh_ * HD, Tn, Tp, dSt, wave, lane);
-    }
+    // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K
+    dma_slice_g(qkv, sb_ * Tn, ld, D + sh_ * HD, Tn, Tp, Ks, wave, lane);
     if (kact && key < Tn) {
       bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD;
       bf16_t* dvr = dkr + D;
@@ -893,6 +1016,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       }
     }
   }
+  // the last item re-staged its own K / Q / dO / V (dead blocks): retire that DMA before the LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1047,6 +1172,16 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
   return vit::check_launch("vit_attn_fwd");
 }
 
+namespace {
+bool bwd_fused(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype) {
+  return use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_BWD_SPLIT);
+}
+}  // namespace
+
+extern "C" int vit_attn_bwd_uses_o32(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype) {
+  return dtype == VIT_BF16 && !bwd_fused(B, T, H, hd, dtype) ? 1 : 0;
+}
+
 extern "C" int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype) {
   if (use_mfma(dtype, hd)) return B * H * T * (int64_t)sizeof(float);
   return 2 * B * H * T * T * (int64_t)sizeof(float);
@@ -1060,20 +1195,16 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
   hipStream_t s = VIT_STREAM(stream);
   const int64_t rows = B * T * H;
   const unsigned dgrid = (unsigned)std::min<int64_t>((rows * 8 + 255) / 256, 16384);
-  if (use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_BWD_SPLIT)) {
-    // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid
+  if (bwd_fused(B, T, H, hd, dtype)) {
+    // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid; delta is
+    // formed in the kernel from P and dP (o and o32 are not read)
     const int64_t items = B * H;
-    const float* dl = nullptr;             // without o32 the kernel computes delta from the bf16 O itself
-    if (o32) {
-      attn_delta<float><<<dgrid, 256, 0, s>>>(o32, (const bf16_t*)d_o, (float*)workspace, B, T, H);
-      dl = (const float*)workspace;
-    }
-    // persistent: one workgroup per CU; VIT_FLAG_SHARED_CUS: one per item (no cross-item prefetch, any free CU)
+    // VIT_FLAG_SHARED_CUS: one workgroup per item (no cross-item prefetch, any free CU)
     int64_t grid = (flags & VIT_FLAG_SHARED_CUS) ? items : std::min<int64_t>(items, vit_cu_count());
     if (const int64_t gopt = vit::opt(vit::OPT_ATTN_BWD_GRID)) grid = std::max<int64_t>(1, std::min<int64_t>(items, gopt));
 #define BWD(NQ)                                                                                                  \
-  attn_bwd_fused<NQ><<<(unsigned)grid, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)o, (const bf16_t*)d_o, lse, \
-                                                    dl, (bf16_t*)dqkv, T, H, items, scale)
+  attn_bwd_fused<NQ><<<(unsigned)grid, 512, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, (bf16_t*)dqkv, T, H, \
+                                                    items, scale)
     switch ((int)((T + 31) / 32)) {
       case 1: BWD(1); break;
       case 2: BWD(2); break;
