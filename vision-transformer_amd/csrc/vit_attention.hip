@@ -583,6 +583,10 @@ constexpr int FB_TMAX = 256;
 #ifndef ATT_KVLDS
 #define ATT_KVLDS 1
 #endif
+#ifndef ATT_ABL_NODELTA           // ablations for A/B builds only (tools/build_variant.sh): wrong results
+#define ATT_ABL_NODELTA 0
+#endif
+
 
 VIT_DEV __amdgpu_buffer_rsrc_t make_rsrc_b(const void* base, int64_t bytes) {
   const uint32_t nrec = bytes >= 0x7fffffffLL ? 0x7fffffffu : (uint32_t)bytes;
@@ -722,19 +726,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   constexpr int QRS = HD + 4;                         // dQ staging row stride (elements)
   constexpr int QST = 32 * QRS;                       // dQ block staging [32][68]
   constexpr int NF = Tp + 2 * 8 * 32 + 8 * 32;        // floats: lse2 [Tp], delta partials [2][8][32], per-wave delta [8][32]
-  constexpr int XS = NQB < 8 ? 32 * 32 : 0;           // dS^T scratch of the wave without a key block
   // V image too when it fits in the 160 KiB (Tp <= 224): staged during the previous item instead of read from global
   // at the top of each item (an exposed load round trip per item)
-  constexpr bool VLDS = (4 * IMG + 2 * DST + 2 * QST + XS) * 2 + NF * 4 <= 160 * 1024;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(VLDS ? 4 : 3) * IMG + 2 * DST + 2 * QST + XS + 2 * NF];
+  constexpr bool VLDS = (4 * IMG + 2 * DST + 2 * QST) * 2 + NF * 4 <= 160 * 1024;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[(VLDS ? 4 : 3) * IMG + 2 * DST + 2 * QST + 2 * NF];
   bf16_t* Ks = smem;
   bf16_t* Qs = Ks + IMG;
   bf16_t* Gs = Qs + IMG;
   bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]
   bf16_t* dQs = dSt + 2 * DST;                         // [2][32][64]
   bf16_t* Vs = dQs + 2 * QST;                          // [Tp][64] when VLDS
-  bf16_t* dSx = Vs + (VLDS ? IMG : 0);                 // [32][32] when NQB < 8
-  float* lse2s = reinterpret_cast<float*>(dSx + XS);
+  float* lse2s = reinterpret_cast<float*>(Vs + (VLDS ? IMG : 0));
   float* dpart = lse2s + Tp;                           // [2][8][32]
   float* dwav = dpart + 2 * 8 * 32;                    // [8][32]
 
@@ -744,9 +746,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   const int64_t D = H * HD, ld = 3 * D;
   const float c2 = scale * LOG2E;
 
-  // Wave w owns key block w.  A wave without one (w >= nqb: wave 7 at T = 197) runs the same instruction stream on
-  // key block 0 with every key masked (P = 0, so dS = 0 and its dK / dV are never stored): no wave-dependent branch
-  // splits the loop body, which the compiler can then schedule as one block.
+  // Wave w owns key block w; a wave without one (w >= nqb: wave 7 at T = 197) skips front / back (a dummy block
+  // with every key masked, to keep the loop body free of wave-dependent branches, measured 7 us slower at C2).
   const bool kact = wave < nqb;
   const int kb = kact ? wave * 32 : 0;
   const int key = kb + (lane & 31);
@@ -828,6 +829,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 
     // front(qb): this wave's key block against query block qb -> P, dV; partial delta -> dpart[qb & 1][wave]
     auto front = [&](int qb) {
+      if (!kact) return;                              // the wave without a key block (measured: cheaper than a masked dummy block)
       const int q0 = qb * 32;
       const bf16_t* Qb = Qs + q0 * HD;
       const bf16_t* Gb = Gs + q0 * HD;
@@ -863,7 +865,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       float t[16], u[8];
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = pc[r] * dpc[r];
+#if ATT_ABL_NODELTA
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = t[j];
+#else
       rowsum32(t, u);
+#endif
       // lane 16R (R = 16-lane row; hf = R >> 1) writes registers 8 (R & 1) + j: queries 16 (R & 1) + 4 hf + 0..3 and
       // 16 (R & 1) + 8 + 4 hf + 0..3
       if ((lane & 15) == 0) {
@@ -875,6 +882,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 
     // back(qb): delta of query block qb (its partials are behind the last barrier) -> dS -> dK; dS^T -> dSt[qb & 1]
     auto back = [&](int qb) {
+      if (!kact) return;
       const int q0 = qb * 32;
       const bf16_t* Qb = Qs + q0 * HD;
       float ds[16];
@@ -908,8 +916,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         dk[db] = mfma32(trd(Qb, tf_off[db][0], tf_off[db][1]), d0, dk[db]);
         dk[db] = mfma32(trd(Qb + 16 * HD, tf_off[db][0], tf_off[db][1]), d1, dk[db]);
       }
-      // (a wave without a key block writes its zero dS^T rows to a scratch block instead of key block 0's)
-      bf16_t* dS = (kact ? dSt + (qb & 1) * DST : dSx) + key * 32;
+      bf16_t* dS = dSt + (qb & 1) * DST + key * 32;
       const int ksw = (key >> 1) & 7;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {                // queries 8 g4 + 4 hf + 0..3: unit 2 g4 + hf
