@@ -401,6 +401,51 @@ def _attn_ref(qkv, B, T, H, hd, scale):
     return o, lse, p
 
 
+@pytest.mark.parametrize("shape", ["proj_fwd", "fc2_fwd", "dgrad_qkv", "fc1_fwd", "dgrad_fc2m"])
+def test_gemm_c2_shapes_tail_split(libopt, shape):
+    """The forward / input-gradient GEMMs at their real C2 shapes (M = 50,432: 591 / 2,364 tiles over 256 CUs, the
+    persistent grid).  With the split-K tail (option gemm_tail, on: N = 768 and K >= 2048 run the last partial round
+    split over K with fp32 slabs) against whole tiles only (gemm_tail 0): the same outputs to bf16 rounding of a
+    different fp32 summation order, identical keep / ReLU bits where the pre-rounding values agree, bitwise run to
+    run, and within bf16 tolerance of an fp32 torch product."""
+    M, D = 256 * 197, 768
+    m, n, k, bkc, kind = {"proj_fwd": (M, D, D, True, "bdr"), "fc2_fwd": (M, D, 4 * D, True, "bdr"),
+                          "dgrad_qkv": (M, D, 3 * D, False, "plain"), "fc1_fwd": (M, 4 * D, D, True, "relu_mask"),
+                          "dgrad_fc2m": (M, 4 * D, D, False, "auxm")}[shape]
+    g = torch.Generator(device=DEV).manual_seed(11)
+    a = (torch.rand(m, k, device=DEV, generator=g) * 2 - 1).bfloat16()
+    b = (torch.rand(n, k, device=DEV, generator=g) * 2 - 1).bfloat16() if bkc else \
+        (torch.rand(k, n, device=DEV, generator=g) * 2 - 1).bfloat16()
+    bias = torch.randn(n, device=DEV, generator=g)
+    res = torch.randn(m, n, device=DEV, generator=g).bfloat16()
+    mask_in = torch.randint(0, 256, (_ops.mask4_bytes(m, n),), device=DEV, generator=g, dtype=torch.uint8)
+    ws = torch.empty(64 << 20, dtype=torch.float32, device=DEV)
+
+    def run():
+        c = torch.empty(m, n, dtype=torch.bfloat16, device=DEV)
+        mask = torch.zeros(_ops.mask4_bytes(m, n), dtype=torch.uint8, device=DEV)
+        kw = {"bdr": dict(bias=bias, dropout_p=0.2, seed=3, res=res, ldres=n, mask_out=mask),
+              "relu_mask": dict(bias=bias, act=_ops.ACT_RELU, mask_out=mask), "auxm": dict(aux=mask_in),
+              "plain": {}}[kind]
+        _ops.gemm(a, b, c, m, n, k, k, k if bkc else n, n, b_kcontig=bkc, workspace=ws, **kw)
+        return c, mask
+
+    c1, m1 = run()
+    c1b, m1b = run()
+    assert torch.equal(c1, c1b) and torch.equal(m1, m1b)                 # deterministic
+    libopt("gemm_tail", 0)
+    c0, m0 = run()
+    ref = a.float() @ (b.float().t() if bkc else b.float())
+    scale = float(ref.abs().max())
+    d = (c1.float() - c0.float()).abs()
+    assert float(d.max()) <= 2 ** -7 * max(scale, 1.0), float(d.max())    # summation order only (bf16 ulps)
+    assert float((d > 0).float().mean()) < 0.02
+    if kind == "plain":
+        assert float((c1.float() - ref).abs().max()) <= 2 ** -7 * scale
+    if kind in ("bdr", "relu_mask"):
+        assert float((m1 != m0).float().mean()) < 1e-3                 # bits flip only where a value sits at 0
+
+
 @pytest.mark.parametrize("dtype,hd", [(torch.float32, 16), (torch.float32, 64), (torch.bfloat16, 64),
                                       (torch.bfloat16, 32)])
 @pytest.mark.parametrize("T", [5, 17, 197, 577])

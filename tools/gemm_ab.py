@@ -3,8 +3,9 @@ cdna_hip_programming.md §5.4 rule 24).  Each build is loaded RTLD_LOCAL, so sev
 
     python tools/gemm_ab.py LIB1.so LIB2.so@VIT_GEMM_GROUP=4 ... [--reps 10] [--shapes fwd_qkv,...]
 
-A build spec may carry `@NAME=VALUE[,NAME=VALUE]`: environment set around that build's calls (runtime switches such as
-VIT_GEMM_GROUP).  Prints the median time per (shape, build) and TF/s; checks outputs bitwise against the first.""" 
+A build spec may carry `@NAME=VALUE[,NAME=VALUE]`: library options (vit_set_option) set around that build's calls,
+e.g. `libvit_hip.so@gemm_tail=0`.  Prints the median time per (shape, build) and TF/s; checks outputs bitwise
+against the first ("=" / "!"), and reports the largest relative difference to it."""  
 import argparse
 import ctypes
 import os
@@ -41,6 +42,9 @@ def load(path):
     lib.vit_gemm_workspace_bytes.restype = ctypes.c_int64
     lib.vit_gemm_split_k_hint.argtypes = [ctypes.c_int64] * 3 + [ctypes.c_int]
     lib.vit_last_error.restype = ctypes.c_char_p
+    lib.vit_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    lib.vit_get_option.argtypes = [ctypes.c_char_p]
+    lib.vit_get_option.restype = ctypes.c_int64
     return lib
 
 
@@ -102,8 +106,9 @@ def main():
         outs = {}
         for rep in range(args.reps + 2):
             for nm, lib, env in zip(names, libs, envs):
-                saved = {kk: os.environ.get(kk) for kk in env}
-                os.environ.update(env)
+                saved = {kk: lib.vit_get_option(kk.encode()) for kk in env} if lib is not None else {}
+                for kk, vv in env.items():
+                    lib.vit_set_option(kk.encode(), int(vv))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 if lib is None:   # "torch": hipBLASLt plain GEMM of the same operands (no epilogue), reference only
                     at = a if akc else a.t()
@@ -119,10 +124,7 @@ def main():
                     e1.record()
                 torch.cuda.synchronize()
                 for kk, vv in saved.items():
-                    if vv is None:
-                        os.environ.pop(kk, None)
-                    else:
-                        os.environ[kk] = vv
+                    lib.vit_set_option(kk.encode(), vv)
                 if rc != 0:
                     sys.exit(f"{nm}: vit_gemm failed: {lib.vit_last_error().decode()}")
                 if rep >= 2:
@@ -133,7 +135,8 @@ def main():
         line = f"{sname:10s} split={split:2d}"
         for nm in names:
             t = sorted(times[nm])[len(times[nm]) // 2]
-            same = "=" if torch.equal(outs[nm], outs[names[0]]) else "!"
+            same = "=" if torch.equal(outs[nm], outs[names[0]]) else \
+                f"!{float((outs[nm].float() - outs[names[0]].float()).abs().max() / outs[names[0]].float().abs().max()):.0e}"
             if nm == "torch":
                 same = "~"
             line += f" | {nm}: {t * 1e6:7.1f}us {flop / t / 1e12:7.1f}TF {same}"
