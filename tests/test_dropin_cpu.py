@@ -133,6 +133,32 @@ def test_train_py_host_path_runs_c1_loop(tmp_path):
     assert line["device"] == "cpu" and line["steps"] == 2 and line["ms_per_step"] > 0
 
 
+def test_train_reference_loop_bookkeeping(tmp_path, monkeypatch):
+    """train(reference_loop=True): validation after EVERY epoch whatever eval_iter says (reference train.py:103,114),
+    the step counter restarting at 0 on resume (:67) and the epoch loss summed on the host from loss.item() (:97-99);
+    the default loop validates every eval_iter epochs and continues the step counter."""
+    import train as T
+    from VisionTransformer import config
+    cfg = config.ViTConfig(3, 4, 4, 32, 16, 2, 1, "cpu", 4)
+    monkeypatch.setattr(T, "device", "cpu")
+    calls = []
+    monkeypatch.setattr(T, "evaluate", lambda model, loader, metric: calls.append(1) or 0.5)
+    ds = T.SyntheticImages(8, 3, 32, 4, seed=3)
+    dl = torch.utils.data.DataLoader(ds, batch_size=4, drop_last=True)
+    loss_ref = T.train(cfg, dl, dl, 2, 5, str(tmp_path / "l1"), str(tmp_path / "ck1"), reference_loop=True)
+    assert len(calls) == 3                                  # epochs 0, 1, 2: every one
+    assert torch.load(tmp_path / "ck1" / "2.pt", weights_only=True)["step"] == 6
+    calls.clear()
+    T.train(cfg, dl, dl, 3, 5, str(tmp_path / "l1"), str(tmp_path / "ck1"), reference_loop=True)   # resumes at 2
+    assert torch.load(tmp_path / "ck1" / "3.pt", weights_only=True)["step"] == 4        # restarted at 0: 2 epochs
+    calls.clear()
+    T.train(cfg, dl, dl, 2, 5, str(tmp_path / "l2"), str(tmp_path / "ck2"))
+    assert len(calls) == 1                                  # epoch 0 only (eval_iter 5)
+    T.train(cfg, dl, dl, 3, 5, str(tmp_path / "l2"), str(tmp_path / "ck2"))
+    assert torch.load(tmp_path / "ck2" / "3.pt", weights_only=True)["step"] == 10       # 6 + 2 epochs x 2 steps
+    assert loss_ref > 0
+
+
 def test_bench_spawns_ranks_dry_run():
     """`bench.py --gpus 2` without torchrun starts 2 ranks itself (spawn; the parent makes no GPU call) and rank 0
     prints one JSON line with n_gpus = 2, dp2, global batch 512 (the driver's --gpus N contract)."""

@@ -233,6 +233,45 @@ def test_layernorm_fwd_bwd(dtype, cols):
     assert torch.equal(drop.float(), dx.float() * keep)
 
 
+@pytest.mark.parametrize("dtype,cols", [(torch.bfloat16, 768), (torch.bfloat16, 1024), (torch.bfloat16, 3072),
+                                        (torch.float32, 768), (torch.float32, 3072)])
+def test_layernorm_bwd_many_rows_and_saved_mask(dtype, cols):
+    """vit_layernorm_bwd at >= 8192 rows (every wave of a block busy, the next 4-row group prefetched, the per-wave LDS
+    accumulators summed in wave order across many row groups; the fp32 NV 6-12 path included) against torch, and the
+    saved-mask form (drop_mask: the forward's keep bits as a mask4, here packed from the same counter hash) bitwise
+    equal to the hash form, dx, drop_out and every partial column sum alike."""
+    from oracle.vit_oracle import dropout_keep
+    torch.manual_seed(cols)
+    rows = 8192 + 36
+    x = (torch.randn(rows, cols, device=DEV) * 2 + 0.5).to(dtype)
+    g = torch.rand(cols, device=DEV) + 0.5
+    b = torch.randn(cols, device=DEV)
+    y, mean, rstd = _ops.layernorm_fwd(x, g, b)
+    dy = torch.randn(rows, cols, device=DEV).to(dtype)
+    dres = torch.randn(rows, cols, device=DEV).to(dtype)
+    xr = x.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (cols,), gr, br, 1e-5).backward(dy.float())
+    dx, drop = torch.empty_like(x), torch.empty_like(x)
+    part = _ops.layernorm_bwd(dy, x, g, mean, rstd, dx, dres=dres, drop_out=drop, drop_p=0.2, drop_seed=7, osum=True)
+    keep = dropout_keep(7, (rows, cols)).to(DEV)
+    mask = _mask4_pack(keep.bool())
+    dx2, drop2 = torch.empty_like(x), torch.empty_like(x)
+    part2 = _ops.layernorm_bwd(dy, x, g, mean, rstd, dx2, dres=dres, drop_out=drop2, drop_p=0.2, drop_seed=7,
+                               osum=True, drop_mask=mask)
+    assert torch.equal(dx, dx2) and torch.equal(drop, drop2) and torch.equal(part, part2)
+    assert torch.equal(drop.float(), dx.float() * keep)
+    dg, db, ds = (torch.empty(cols, device=DEV) for _ in range(3))
+    _ops.colsum_finish(part, [dg, db, ds])
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    ref_dx = xr.grad + dres.float()
+    assert (dx.float() - ref_dx).abs().max().item() <= tol * 4 * ref_dx.abs().max().item()
+    assert (dg - gr.grad).abs().max().item() <= tol * 4 * gr.grad.abs().max().item()
+    assert (db - br.grad).abs().max().item() <= tol * 4 * br.grad.abs().max().item()
+    ref_ds = drop.double().sum(0) * 1.25
+    assert ((ds.double() - ref_ds).abs() <= 1e-5 * drop.double().abs().sum(0) + 1e-6).all()
+
+
 @pytest.mark.parametrize("variant", ["plain", "aux", "bias_relu", "bias_drop_res", "f32_out", "v2_small"])
 def test_gemm_colsum_part(variant):
     """Column sums of C as stored, fused into the v4 row epilogue (a separate pass for the other kernels / general

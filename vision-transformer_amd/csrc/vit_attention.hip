@@ -1037,33 +1037,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 // workgroups share a CU, so one's DMA prologue overlaps the other's loop.  O leaves registers as 16-B row pieces: a
 // permlane32 half swap pairs the two 8-B column groups a row is split over (cdna_hip_programming.md T21).
 // ---------------------------------------------------------------------------------------------------------------
+// One wave's 32 queries (q0 = 32 * wave) of one (image, head) against the NKB key blocks of the K / V images: the
+// online softmax of attn_fwd_mfma, then O (bf16, 16-B row pieces), optionally O unrounded (o32) and the LSE.
 template <int NKB>
-__global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
-                                                           float* __restrict__ o32, float* __restrict__ lse,
-                                                           int64_t Tn64, int64_t H, float scale) {
+VIT_DEV void fwd_queries(const bf16_t* Ks, const bf16_t* Vs, const bf16x8_t (&qf)[4], int wave, int lane, int Tn,
+                         float c2, bf16_t* __restrict__ o, float* __restrict__ o32, float* __restrict__ lse, int64_t b,
+                         int64_t h, int64_t bh, int64_t D) {
   constexpr int Tp = NKB * 32;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * Tp * HD];
-  bf16_t* Ks = smem;
-  bf16_t* Vs = smem + Tp * HD;
-  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int Tn = (int)Tn64;
-  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
-  const int64_t D = H * HD, ld = 3 * D;
-  const float c2 = scale * LOG2E;
-  {
-    const int64_t nb = gridDim.x / H;                  // host guarantees the tensor is < 2 GiB
-    const __amdgpu_buffer_rsrc_t rq = make_rsrc_b(qkv, nb * Tn * ld * 2);
-    dma_head_slice(rq, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane, NKB);
-    dma_head_slice(rq, b * Tn, ld, 2 * D + h * HD, Tn, Tp, Vs, wave, lane, NKB);
-  }
+  const int hf = lane >> 5;
   const int q0 = wave * 32;
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = glb_frag(qkv + b * Tn * ld, ld, q0, Tn, h * HD, s, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
   f32x16 oacc[2] = {f32x16{}, f32x16{}};
   float m_run = -INFINITY, l_run = 0.f;
 #pragma unroll
@@ -1101,7 +1083,7 @@ __global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restr
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = 1.0f / l_tot;
   const int q = q0 + (lane & 31);
-  if (o32 && q < Tn) {                               // fp32 O for the backward's delta (training forward only)
+  if (o32 && q < Tn) {                               // fp32 O for the tiled backward's delta
     float* orow32 = o32 + (b * Tn + q) * D + h * HD + 4 * hf;
 #pragma unroll
     for (int db = 0; db < 2; ++db)
@@ -1135,6 +1117,33 @@ __global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restr
     if (q < Tn) *reinterpret_cast<uint4*>(orow + 8 * k) = make_uint4(pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]);
   }
   if (q < Tn && hf == 0) lse[bh * Tn + q] = (m_run + log2f(l_tot)) / LOG2E;
+}
+
+template <int NKB>
+__global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                           float* __restrict__ o32, float* __restrict__ lse,
+                                                           int64_t Tn64, int64_t H, float scale) {
+  constexpr int Tp = NKB * 32;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * Tp * HD];
+  bf16_t* Ks = smem;
+  bf16_t* Vs = smem + Tp * HD;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Tn = (int)Tn64;
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * HD, ld = 3 * D;
+  {
+    const int64_t nb = gridDim.x / H;                  // host guarantees the tensor is < 2 GiB
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc_b(qkv, nb * Tn * ld * 2);
+    dma_head_slice(rq, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane, NKB);
+    dma_head_slice(rq, b * Tn, ld, 2 * D + h * HD, Tn, Tp, Vs, wave, lane, NKB);
+  }
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = glb_frag(qkv + b * Tn * ld, ld, wave * 32, Tn, h * HD, s, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  fwd_queries<NKB>(Ks, Vs, qf, wave, lane, Tn, scale * LOG2E, o, o32, lse, b, h, bh, D);
 }
 
 bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }

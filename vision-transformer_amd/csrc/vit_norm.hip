@@ -95,8 +95,12 @@ template <> struct Raw4<float> {
 template <class T> VIT_DEV float as_stored(float v) { return sizeof(T) == 2 ? bf2f(f2bf(v)) : v; }
 
 // AL (accumulators in LDS): the per-column dgamma / dbeta / output sums of each wave live in its own LDS region instead
-// of 3 x 4 x NV registers per lane, which takes the kernel from 3 to 4 waves per SIMD without spills (one more row of
-// loads in flight per SIMD); each lane only ever touches its own columns, so the row loop needs no barrier.
+// of 3 x 4 x NV registers per lane; each lane only ever touches its own columns, so the row loop needs no barrier.
+// LDS per 256-thread block is 13 KiB x NV (red[4][3][256 NV] + gamma), so the occupancy it allows is NV-dependent:
+// D = 768 (NV 3, 39 KiB): 4 blocks = 4 waves per SIMD, the register form's 3 without spills (one more row of loads in
+// flight per SIMD; the measured gain); D = 1024 (NV 4, 52 KiB): 3 blocks = 3 waves per SIMD; NV 6-12
+// (78-156 KiB: the head's LN(4D) rows): 1-2 blocks.  The wide fp32 rows use it because their register form spilled
+// ~350 VGPRs (209 -> 26.5 us); the bf16 NV 4-12 shapes are not on the C2 step (ViT-L's D = 1024 is: 3 waves / SIMD).
 template <class T, int NV, bool AL>
 __global__ __launch_bounds__(256, AL && NV <= 4 ? 4 : 1) void ln_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ x,
                                                      int64_t ldx, const float* __restrict__ gamma,

@@ -105,8 +105,14 @@ def _rank_world():
 
 
 def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkpoint_dir, lr=1e-4,
-          log_every=1, max_steps=None):
-    """The reference training loop (train.py:60-119) on the HIP path.  Returns the last epoch's summed loss."""
+          log_every=1, max_steps=None, reference_loop=False):
+    """The reference training loop (train.py:60-119) on the HIP path.  Returns the last epoch's summed loss.
+
+    Defaults keep the GPU busy: the epoch loss is summed on the device, validation runs every `eval_iter` epochs and a
+    resumed run continues its step counter.  `reference_loop=True` restores the reference's bookkeeping exactly:
+    validation after every epoch (its eval_iter gate is commented out, train.py:114), `iteration` restarting at 0 on
+    resume (train.py:67; the checkpoint's `step` is not read back) and the epoch loss as the host sum of each step's
+    loss.item() (train.py:97-99: one host sync per step)."""
     rank, world = _rank_world()
     saved_epoch = search_checkpoint(checkpoint_dir)
     torch.manual_seed(0)                              # identical init on every rank
@@ -120,7 +126,7 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
         model = model.to(device)
         optimizer = make_optimizer(model.parameters(), lr=lr, weight_decay=1e-4, device=device)
         optimizer.load_state_dict(ckpt["optimizer_state_dict"])
-        iteration = int(ckpt.get("step", 0))
+        iteration = 0 if reference_loop else int(ckpt.get("step", 0))
     else:
         saved_epoch = 0
         model = model.to(device)
@@ -134,6 +140,7 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
     running_loss = 0.0
     for epoch in range(saved_epoch, epochs + 1):
         loss_sum = torch.zeros((), device=device)
+        host_loss = 0.0
         t0 = time.time()
         nb = 0
         for tensors, labels in train_loader:
@@ -144,17 +151,20 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
             optimizer.zero_grad(set_to_none=True)
             loss.backward()
             optimizer.step()
-            loss_sum += loss.detach()
+            if reference_loop:
+                host_loss += loss.item()
+            else:
+                loss_sum += loss.detach()
             if writer is not None and log_every and iteration % log_every == 0:
                 writer.add_scalar("Loss/train_batch", loss.item(), iteration)
             iteration += 1
             nb += 1
             if max_steps and nb >= max_steps:
                 break
-        running_loss = float(loss_sum.item())
+        running_loss = host_loss if reference_loop else float(loss_sum.item())
         dt = time.time() - t0
         acc = None
-        if test_loader is not None and eval_iter and epoch % eval_iter == 0:
+        if test_loader is not None and (reference_loop or (eval_iter and epoch % eval_iter == 0)):
             from sklearn.metrics import accuracy_score
             acc = round(float(evaluate(model, test_loader, accuracy_score)), 2)
             if writer is not None:
@@ -211,6 +221,9 @@ def main():
     ap.add_argument("--test-size", type=int, default=64)
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--eval-iter", type=int, default=1)
+    ap.add_argument("--reference-loop", action="store_true",
+                    help="the reference's loop bookkeeping exactly: validate every epoch, restart the step counter on "
+                         "resume, host-summed loss (train.py:60-119)")
     ap.add_argument("--data", default="synthetic", choices=["synthetic", "synthetic-u8", "cifar10-bin", "folder"],
                     help="synthetic: N(0,1) float images at --img; the others decode uint8 images and apply the "
                          "reference transform (GPU kernel on cuda, Pillow on cpu)")
@@ -270,11 +283,11 @@ def main():
     sampler = torch.utils.data.DistributedSampler(train_set) if world > 1 else None
     if args.data != "synthetic" and device == "cuda":
         from VisionTransformer import data as D
-        tf = D.GpuImageTransform(args.img)
+        # one transform (and coefficient workspace) per loader: each stages its batches on its own side stream
         train_loader = D.DeviceBatches(D.raw_loader(train_set, args.batch, shuffle=True, num_workers=args.workers,
-                                                    sampler=sampler), tf, device)
+                                                    sampler=sampler), D.GpuImageTransform(args.img), device)
         test_loader = D.DeviceBatches(D.raw_loader(test_set, args.batch, shuffle=False, num_workers=args.workers),
-                                      tf, device)
+                                      D.GpuImageTransform(args.img), device)
     else:
         if args.data != "synthetic":
             from VisionTransformer import data as D
@@ -285,7 +298,7 @@ def main():
         test_loader = torch.utils.data.DataLoader(test_set, batch_size=args.batch, num_workers=args.workers,
                                                   drop_last=True, pin_memory=pin)
     train(cfg, train_loader, test_loader, args.epochs, args.eval_iter, args.log_dir, args.checkpoint_dir,
-          lr=args.lr, max_steps=args.steps)
+          lr=args.lr, max_steps=args.steps, reference_loop=args.reference_loop)
     if world > 1:
         dist.destroy_process_group()
 
