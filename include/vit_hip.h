@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 10
+#define VIT_ABI_VERSION 11
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -203,6 +203,16 @@ int vit_colsum(const void* x, int64_t ldx, int32_t dtype, int64_t rows, int64_t 
                float beta, void* workspace, void* stream);
 int vit_colsum_finish(const float* part, int64_t nparts, int64_t cols, int32_t nsets, float* out0, float* out1,
                       float* out2, float beta, void* stream);
+/* vit_colsum_finish_batch: up to 8 vit_colsum_finish jobs in one launch (the bias / LN-affine gradients of one encoder
+ * block), each job's result bitwise that of its own vit_colsum_finish. */
+typedef struct {
+  const float* part;  /* [nsets][nparts][cols] */
+  int64_t nparts, cols;
+  int32_t nsets;      /* 1..3 */
+  float* out[3];
+  float beta;
+} vit_colsum_job;
+int vit_colsum_finish_batch(const vit_colsum_job* jobs, int32_t njobs, void* stream);
 int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,
                int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
                void* stream);

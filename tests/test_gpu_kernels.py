@@ -576,6 +576,24 @@ def test_attention_probs_generic():
     assert (probs - p).abs().max().item() < 1e-5
 
 
+def test_colsum_finish_batch_matches_single():
+    """vit_colsum_finish_batch (one launch for an encoder block's bias / LN-affine gradient sums) gives each job's
+    outputs bitwise as its own vit_colsum_finish, beta included."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    jobs = [(197, 3072, 1, 0.0), (1576, 768, 3, 1.0), (1576, 768, 2, 0.5), (3, 100, 1, 0.0)]
+    parts = [torch.randn(ns, nparts, cols, device=DEV, generator=g) for nparts, cols, ns, _ in jobs]
+    init = [[torch.randn(cols, device=DEV, generator=g) for _ in range(ns)] for _, cols, ns, _ in jobs]
+    single = [[t.clone() for t in outs] for outs in init]
+    for p, outs, (_, _, _, beta) in zip(parts, single, jobs):
+        _ops.colsum_finish(p, outs, beta=beta)
+    batch = [[t.clone() for t in outs] for outs in init]
+    _ops.colsum_finish_batch([(p, outs, beta) for p, outs, (_, _, _, beta) in zip(parts, batch, jobs)])
+    for a, b in zip(single, batch):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    assert torch.allclose(single[0][0], parts[0][0].double().sum(0).float(), rtol=1e-5, atol=1e-4)
+
+
 def test_misc_kernels():
     torch.manual_seed(6)
     # im2col (vit.py:21-29 conv as GEMM)

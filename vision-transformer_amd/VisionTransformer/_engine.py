@@ -636,7 +636,7 @@ class Engine:
             self._gemm_rows(pr, g1, self.ww[f"{l}.fc2_w"], dh, R, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
                             colsum_part=dh_part, alpha=gs, shared_cus=self.shared_cus)
             mk("gemm_dgrad", 1)
-            _ops.colsum_finish(dh_part, [gw[f"{l}.fc1_b"]], beta=beta)
+            cs_jobs = [(dh_part, [gw[f"{l}.fc1_b"]], beta)]      # this block's bias / LN-affine sums: one launch below
             if req[f"{l}.fc1_w"]:
                 self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, R, 4 * D, D, beta, side, "gemm_wgrad")
             da2 = torch.empty(R, D, dtype=dt, device=dev)
@@ -652,7 +652,7 @@ class Engine:
             part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx, drop_out=g0,
                                       drop_p=DROPOUT_P, drop_mask=pm, osum=True)
             mk("ln_bwd", 1)
-            _ops.colsum_finish(part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta=beta)
+            cs_jobs.append((part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta))
             if g0 is None:
                 g0 = dx_mid
             # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
@@ -693,7 +693,8 @@ class Engine:
                                       osum=l > 0)
             mk("ln_bwd", 1)
             outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if l > 0 else [])
-            _ops.colsum_finish(part, outs, beta=beta)
+            cs_jobs.append((part, outs, beta))
+            _ops.colsum_finish_batch(cs_jobs)
             g1_summed = l > 0
             self._bucket_ready(self.block_range[l], side)
             dx = dx_in

@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 F32, BF16, MASK4 = 0, 1, 2
 FLAG_SHARED_CUS = 1          # VIT_FLAG_SHARED_CUS (vit_hip.h)
@@ -39,6 +39,11 @@ class GemmDesc(ctypes.Structure):
         ("dropout_row_stride", ctypes.c_int64),
         ("flags", ctypes.c_int32),
     ]
+
+
+class ColsumJob(ctypes.Structure):
+    _fields_ = [("part", ctypes.c_void_p), ("nparts", ctypes.c_int64), ("cols", ctypes.c_int64),
+                ("nsets", ctypes.c_int32), ("out", ctypes.c_void_p * 3), ("beta", ctypes.c_float)]
 
 
 class TensorChunk(ctypes.Structure):
@@ -71,6 +76,7 @@ _SIGS = {
     "vit_colsum_workspace_bytes": (_I64, [_I64, _I64]),
     "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _F, _P, _P]),
     "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),
+    "vit_colsum_finish_batch": (ctypes.c_int, [ctypes.POINTER(ColsumJob), _I32, _P]),
     "vit_copy2d": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _I32, _I64, _I64, _I64, _I64, _F, _P]),
     "vit_dropout_bwd": (ctypes.c_int, [_P, _P, _I32, _I64, _F, _U32, _F, _P]),
     "vit_mask4_apply": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _I32, _P, _I64, _I64, _F, _P]),

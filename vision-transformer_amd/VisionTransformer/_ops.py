@@ -225,6 +225,27 @@ def colsum_finish(part, outs, beta=0.0, stream=None):
     return outs
 
 
+def colsum_finish_batch(jobs, stream=None):
+    """Several colsum_finish jobs [(part, outs, beta), ...] (<= 8) in one launch; each job's outputs are bitwise what
+    colsum_finish(part, outs, beta) gives."""
+    if not 1 <= len(jobs) <= 8:
+        raise ValueError("colsum_finish_batch: 1..8 jobs")
+    arr = (_lib.ColsumJob * len(jobs))()
+    for i, (part, outs, beta) in enumerate(jobs):
+        p3 = part if part.dim() == 3 else part.unsqueeze(0)
+        n = len(outs)
+        if not 1 <= n <= min(3, p3.shape[0]) or not p3.is_contiguous() or p3.dtype != torch.float32:
+            raise ValueError(f"colsum_finish_batch: job {i}: {n} outputs for {p3.shape[0]} partial sets")
+        for t in outs:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != p3.shape[2]:
+                raise ValueError("colsum_finish_batch: outputs must be contiguous float32 of length cols")
+        arr[i].part, arr[i].nparts, arr[i].cols, arr[i].nsets = _ptr(p3), p3.shape[1], p3.shape[2], n
+        for s_, t in enumerate(outs):
+            arr[i].out[s_] = _ptr(t)
+        arr[i].beta = beta
+    _lib.call("vit_colsum_finish_batch", arr, len(jobs), _stream(stream))
+
+
 def copy2d(src, lds, dst, ldd, rows, cols, group=(0, 0), beta=0.0, stream=None):
     _lib.call("vit_copy2d", _ptr(src), lds, dtype_code(src), _ptr(dst), ldd, dtype_code(dst), rows, cols, group[0],
               group[1], beta, _stream(stream))

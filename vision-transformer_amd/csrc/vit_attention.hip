@@ -583,6 +583,12 @@ constexpr int FB_TMAX = 256;
 #ifndef ATT_KVLDS
 #define ATT_KVLDS 1
 #endif
+#ifndef ATT_ORDER                // A/B builds only: loop-body order (0 back, front, dq; 1 front, back, dq; 2 dq first)
+#define ATT_ORDER 0
+#endif
+#ifndef ATT_PRIO                 // A/B builds only: s_setprio 1 around the S / dP MFMA chain
+#define ATT_PRIO 0
+#endif
 #ifndef ATT_ABL_NODELTA           // ablations for A/B builds only (tools/build_variant.sh): wrong results
 #define ATT_ABL_NODELTA 0
 #endif
@@ -841,9 +847,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 #else
         const bf16x8_t kfs = kf[s], vfs = vf[s];
 #endif
+        if (ATT_PRIO && s == 0) __builtin_amdgcn_s_setprio(1);
         sacc = mfma32(rrd(Qb, rf_off[s]), kfs, sacc);             // S[q][key]: lane = key
         pacc = mfma32(rrd(Gb, rf_off[s]), vfs, pacc);             // dP[q][key]
       }
+      if (ATT_PRIO) __builtin_amdgcn_s_setprio(0);
       // registers 4g..4g+3 <-> queries q0 + 8g + 4hf + 0..3: broadcast b128 reads of lse2
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -973,10 +981,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       lds_barrier();
 #pragma unroll 1
       for (int it = 3; it < nqb; ++it) {
+#if ATT_ORDER == 1
+        dq_store(it - 3);
+        front(it);
+        back(it - 1);
+        dq(it - 2);
+#elif ATT_ORDER == 2
+        dq_store(it - 3);
+        dq(it - 2);
+        back(it - 1);
+        front(it);
+#else
         dq_store(it - 3);
         back(it - 1);
         front(it);
         dq(it - 2);
+#endif
         prefetch(it - 2);
         lds_barrier();                                // LDS only: the prefetch and the dQ stores stay in flight
       }

@@ -165,13 +165,12 @@ constexpr int CS2_WAVES = 16;
 struct OutSet {
   float* p[3];
 };
-__global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2(const float* __restrict__ part, int64_t nchunks,
-                                                                int64_t cols, OutSet outs, float beta) {
-  __shared__ float red[CS2_WAVES][64];
+// One 64-column block of one set: the chunk partials summed by 16 waves (8 independent chains per lane), then the wave
+// sums in wave order through LDS.
+VIT_DEV void colsum_block(const float* __restrict__ part, int64_t nchunks, int64_t cols, float* __restrict__ out,
+                          float beta, int64_t cblock, float (*red)[64]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
-  part += (int64_t)blockIdx.y * nchunks * cols;
-  float* __restrict__ out = blockIdx.y == 0 ? outs.p[0] : (blockIdx.y == 1 ? outs.p[1] : outs.p[2]);
+  const int64_t c = cblock * 64 + lane;
   // 8 independent chains per lane (chunk k goes to chain (k / CS2_WAVES) % 8): 8 loads in flight per lane, order fixed
   constexpr int CH = 8;
   float sc[CH];
@@ -195,6 +194,32 @@ __global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2(const float* __r
     for (int i = 0; i < CS2_WAVES; ++i) s += red[i][lane];
     out[c] = beta != 0.f ? beta * out[c] + s : s;
   }
+}
+
+__global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2(const float* __restrict__ part, int64_t nchunks,
+                                                                int64_t cols, OutSet outs, float beta) {
+  __shared__ float red[CS2_WAVES][64];
+  float* out = blockIdx.y == 0 ? outs.p[0] : (blockIdx.y == 1 ? outs.p[1] : outs.p[2]);
+  colsum_block(part + (int64_t)blockIdx.y * nchunks * cols, nchunks, cols, out, beta, blockIdx.x, red);
+}
+
+// vit_colsum_finish_batch: several finishes in one launch; block b belongs to the job whose [first, first + nsets *
+// colblocks) range holds it.  Each (job, set, column block) is the same computation as colsum_stage2's.
+constexpr int CS_BATCH_MAX = 8;
+struct CsBatch {
+  vit_colsum_job job[CS_BATCH_MAX];
+  int64_t first[CS_BATCH_MAX + 1];
+  int n;
+};
+__global__ __launch_bounds__(64 * CS2_WAVES) void colsum_stage2_batch(CsBatch tab) {
+  __shared__ float red[CS2_WAVES][64];
+  const int64_t b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < tab.n && b >= tab.first[j + 1]) ++j;
+  const vit_colsum_job& jb = tab.job[j];
+  const int64_t cbs = (jb.cols + 63) / 64, local = b - tab.first[j], set = local / cbs;
+  float* out = set == 0 ? jb.out[0] : (set == 1 ? jb.out[1] : jb.out[2]);
+  colsum_block(jb.part + set * jb.nparts * jb.cols, jb.nparts, jb.cols, out, jb.beta, local % cbs, red);
 }
 
 int64_t colsum_chunks(int64_t rows, int64_t cols) {
@@ -438,6 +463,24 @@ extern "C" int vit_colsum_finish(const float* part, int64_t nparts, int64_t cols
   dim3 grid((unsigned)((cols + 63) / 64), (unsigned)nsets);
   colsum_stage2<<<grid, 64 * CS2_WAVES, 0, VIT_STREAM(stream)>>>(part, nparts, cols, outs, beta);
   return vit::check_launch("vit_colsum_finish");
+}
+
+extern "C" int vit_colsum_finish_batch(const vit_colsum_job* jobs, int32_t njobs, void* stream) {
+  VIT_REQUIRE(jobs && njobs >= 1 && njobs <= CS_BATCH_MAX, "vit_colsum_finish_batch: 1..%d jobs", CS_BATCH_MAX);
+  CsBatch tab{};
+  tab.n = njobs;
+  tab.first[0] = 0;
+  for (int j = 0; j < njobs; ++j) {
+    const vit_colsum_job& jb = jobs[j];
+    VIT_REQUIRE(jb.part && jb.nparts > 0 && jb.cols > 0 && jb.nsets >= 1 && jb.nsets <= 3,
+                "vit_colsum_finish_batch: bad job %d", j);
+    for (int i = 0; i < jb.nsets; ++i)
+      VIT_REQUIRE(jb.out[i] != nullptr, "vit_colsum_finish_batch: job %d output %d is NULL", j, i);
+    tab.job[j] = jb;
+    tab.first[j + 1] = tab.first[j] + jb.nsets * ((jb.cols + 63) / 64);
+  }
+  colsum_stage2_batch<<<(unsigned)tab.first[njobs], 64 * CS2_WAVES, 0, VIT_STREAM(stream)>>>(tab);
+  return vit::check_launch("vit_colsum_finish_batch");
 }
 
 extern "C" int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void* dst, int64_t ldd, int32_t dst_dtype,
