@@ -187,6 +187,24 @@ def test_library_exports_every_header_symbol():
     assert lib.vit_abi_version() == _lib.ABI_VERSION
 
 
+def test_host_abi_checker_c(tmp_path):
+    """tests/host_abi_check.c, a plain-C host of the C-ABI (gcc, no GPU): version, options, error strings, the
+    argument validation of the entry points and the host helpers.  tools/asan_host_check.sh runs the same program
+    against an AddressSanitizer build of the library's host code (log: profiles/r3_asan_host_check.log)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    libdir = os.path.join(ROOT, "vision-transformer_amd", "VisionTransformer")
+    exe = str(tmp_path / "host_abi_check")
+    subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "host_abi_check.c"), "-o", exe, "-L", libdir, "-lvit_hip",
+                    "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{libdir}", "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout
+
+
 def test_library_options_host_only():
     """vit_set_option / vit_get_option (vit_hip.h): the documented names and shipped defaults, set/restore, and an
     unknown name refused — host-side only, and the library never reads the environment (no getenv in csrc/)."""
