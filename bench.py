@@ -280,6 +280,8 @@ def run(args, rank, world, local):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    if args.roctx and not args.dry_run:
+        model.hip_engine.trace_ranges = True
     log(f"rank {rank}/{world}: warmup {args.warmup} steps")
     for _ in range(args.warmup):
         loss = step()
@@ -433,6 +435,8 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events (profiling runs)")
+    ap.add_argument("--roctx", action="store_true",
+                    help="roctx ranges per kernel family (rocprofv3 --marker-trace timelines; costs host time)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo stand-in step: tests rank launch without a GPU")
     args = ap.parse_args(argv)
 

@@ -205,6 +205,25 @@ def test_host_abi_checker_c(tmp_path):
     assert "all checks passed" in r.stdout
 
 
+def test_engine_roctx_ranges(monkeypatch):
+    """engine.trace_ranges: every marked launch is bracketed by a roctx range named by its kernel family
+    (torch.cuda.nvtx is roctx on ROCm; bench.py --roctx), balanced push / pop; off by default."""
+    from VisionTransformer import _engine
+    calls = []
+    monkeypatch.setattr(torch.cuda.nvtx, "range_push", lambda name: calls.append(("push", name)))
+    monkeypatch.setattr(torch.cuda.nvtx, "range_pop", lambda: calls.append(("pop", None)))
+    eng = _engine.Engine.__new__(_engine.Engine)
+    eng.profile_hook, eng.trace_ranges = None, False
+    eng._mark("gemm_fwd", 0)
+    eng._mark("gemm_fwd", 1)
+    assert calls == []
+    eng.trace_ranges = True
+    for fam in ("gemm_fwd", "attn_bwd"):
+        eng._mark(fam, 0, 1.0, 2.0)
+        eng._mark(fam, 1)
+    assert calls == [("push", "gemm_fwd"), ("pop", None), ("push", "attn_bwd"), ("pop", None)]
+
+
 def test_library_options_host_only():
     """vit_set_option / vit_get_option (vit_hip.h): the documented names and shipped defaults, set/restore, and an
     unknown name refused — host-side only, and the library never reads the environment (no getenv in csrc/)."""

@@ -124,6 +124,9 @@ class Engine:
         # callable(family, phase, flop, nbytes) around the hot launches (bench.py's live HIP-event roofline):
         # phase 0 before the launch with its algorithmic FLOPs / HBM bytes, phase 1 after it, same stream
         self.profile_hook = None
+        # roctx ranges named by kernel family around the same launches (torch.cuda.nvtx is roctx on ROCm): visible in
+        # `rocprofv3 --marker-trace` timelines.  Off by default (a host call per launch).
+        self.trace_ranges = False
         # weight-gradient GEMMs on a side stream (an attribute for A/B runs and tests).  Off by default: measured on
         # ViT-B/16 B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms).
         self.concurrent_wgrad = False
@@ -306,6 +309,11 @@ class Engine:
         h = self.profile_hook
         if h is not None:
             h(fam, phase, flop, nbytes)
+        if self.trace_ranges:
+            if phase == 0:
+                torch.cuda.nvtx.range_push(fam)
+            else:
+                torch.cuda.nvtx.range_pop()
 
     def _wgrad(self, dy, x, out, m, n, k, ld_dy, ld_x, beta, side=None, fam=None, alpha=1.0):
         """out[m][n] (+)= alpha sum_r dy[r][i] x[r][j]: weight gradient, reduction over B*T rows, split-K.  With `side`
