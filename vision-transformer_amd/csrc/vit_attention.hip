@@ -240,15 +240,33 @@ VIT_DEV f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 // row index (within a 32-row MFMA tile) of accumulator register r for lane half h
 VIT_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// XCD-aware (block, head) of a tiled kernel (1-D grid of nblk x B*H workgroups).  Workgroups are dealt round-robin
+// over the 8 XCDs (linear id % 8), each with its own L2; the nblk 128-row blocks of one (image, head) all stream the
+// head's whole K / V (or Q / dO), so in launch order they sat on nblk different XCDs and each fetched the head slice
+// from beyond L2 (C5 PMC: 3.5-3.7x the algorithmic bytes).  Bijective remap: XCD x runs a contiguous range of logical
+// tiles, tile j = (head j / nblk, block j % nblk), so a head's blocks share one L2 and run at about the same time.
+#ifndef ATT_XCD                  // A/B builds only: 0 = launch order
+#define ATT_XCD 1
+#endif
+VIT_DEV void xcd_block(int64_t nblk, int64_t& blk, int64_t& bh) {
+  const int64_t orig = blockIdx.x, nwg = gridDim.x;
+  const int64_t xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int64_t j = ATT_XCD ? (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8 : orig;
+  bh = j / nblk;
+  blk = j - bh * nblk;
+}
+
 __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
                                                      float* __restrict__ o32, float* __restrict__ lse, int64_t Tn,
                                                      int64_t H, float scale) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];  // [buf][K,V]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  int64_t blk, bh;
+  xcd_block((Tn + 127) / 128, blk, bh);
+  const int64_t b = bh / H, h = bh % H;
   const int64_t D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + b * Tn * ld;
-  const int64_t q0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const int64_t q0 = blk * 128 + wave * 32;
   const float c2 = scale * LOG2E;
 
   bf16x8_t qf[4];
@@ -276,6 +294,8 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = sub * 32;
+      // an all-padding key block (T = 577: keys 608..639) adds nothing; a wave whose queries are all >= T stores nothing
+      if ((int64_t)t * KT + kb >= Tn || q0 >= Tn) continue;
       f32x16 sacc = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) sacc = mfma32(row_frag(Ks, kb, s, lane), qf[s], sacc);
@@ -368,10 +388,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
                                                         bf16_t* __restrict__ dqkv, int64_t Tn, int64_t H, float scale) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  int64_t blk, bh;
+  xcd_block((Tn + 127) / 128, blk, bh);
+  const int64_t b = bh / H, h = bh % H;
   const int64_t D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + b * Tn * ld;
-  const int64_t q0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const int64_t q0 = blk * 128 + wave * 32;
   const int64_t q = q0 + (lane & 31);
   const float c2 = scale * LOG2E;
   bf16x8_t qf[4], gf[4];
@@ -459,11 +481,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   // [buf][-lse / scale, -delta] per query: the initial S / dP accumulators (rows >= T: -inf -> P = 0)
   __shared__ __attribute__((aligned(16))) float stat[2][2][KT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / H, h = bh % H;
+  int64_t blk, bh;
+  xcd_block((Tn + 127) / 128, blk, bh);
+  const int64_t b = bh / H, h = bh % H;
   const int64_t D = H * HD, ld = 3 * D;
   const bf16_t* base = qkv + b * Tn * ld;
   const bf16_t* gbase = d_o + b * Tn * D;
-  const int64_t k0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  const int64_t k0 = blk * 128 + wave * 32;
   const float c2 = scale * LOG2E;
   bf16x8_t kf[4], vf[4];
 #pragma unroll
@@ -505,6 +529,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int qb = sub * 32;
+      if ((int64_t)t * KT + qb >= Tn || k0 >= Tn) continue;   // all-padding query block (P = 0) or key wave
       // row constants as the initial accumulators: S' = S - lse / scale, dP' = dP - delta (registers 4g..4g+3 <->
       // queries qb + 8g + 4hf + 0..3: b128 broadcast reads)
       f32x16 sacc, pacc;
@@ -1191,7 +1216,7 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
       }
 #undef FWD
     } else {
-      dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
+      const unsigned grid = (unsigned)(((T + 127) / 128) * B * H);   // 1-D: xcd_block() maps it
       attn_fwd_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, scale);
     }
   } else {
@@ -1256,7 +1281,7 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
     float* delta = (float*)workspace;
     if (o32) attn_delta<float><<<dgrid, 256, 0, s>>>(o32, (const bf16_t*)d_o, delta, B, T, H);
     else attn_delta<bf16_t><<<dgrid, 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)d_o, delta, B, T, H);
-    dim3 grid((unsigned)((T + 127) / 128), (unsigned)(B * H));
+    const unsigned grid = (unsigned)(((T + 127) / 128) * B * H);   // 1-D: xcd_block() maps it
     attn_bwd_dq_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
                                           scale);
     attn_bwd_dkdv_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
