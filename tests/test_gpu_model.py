@@ -313,7 +313,7 @@ def test_side_stream_weight_gradients_bitwise_equal():
 def test_long_sequence_384_vs_oracle(dtype):
     """BASELINE config 5's sequence length (384^2 / patch 16 -> 576 patches + cls = 577 tokens) at reduced width
     (D=128, H=2, hd=64, L=1, B=2): T > 256 takes the tiled attention kernels (attn_fwd_mfma, attn_bwd_dq_mfma,
-    attn_bwd_dkdv_mfma, attn_delta), not the single-workgroup fused ones.  fp32: logits 1e-4, grads 2e-4 (scaled);
+    attn_bwd_dkdv_mfma; delta in the dQ kernel), not the single-workgroup fused ones.  fp32: logits 1e-4, grads 2e-4 (scaled);
     bf16: the same gate as test_bf16_vs_oracle_same_rounding."""
     ocfg = O.make_config("micro", img=384, batch=2, blocks=1)
     ocfg.embedding_size, ocfg.num_heads = 128, 2

@@ -60,7 +60,7 @@ def main():
     ws = torch.empty(_ops.attn_bwd_workspace_bytes(B, T, H, hd, torch.bfloat16) // 4 + 1, device="cuda")
     dq = torch.empty_like(qkv)
     t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=dq, workspace=ws, o32=o32), args.reps)
-    print(f"attn bwd ({'tiled + attn_delta' if uses_o32 else 'fused, in-kernel delta'})  {t:8.1f} us  "
+    print(f"attn bwd ({'tiled, delta in the dQ kernel' if uses_o32 else 'fused, in-kernel delta'})  {t:8.1f} us  "
           f"{fl_b / t / 1e6:7.1f} TF (10 T^2 hd per head)")
     nb = 4
     ref = ref_grads(qkv, d_o, B, T, H, hd, scale, nb)
@@ -74,7 +74,7 @@ def main():
             _ops.attn_fwd(qkv, B, T, H, hd, scale, o32=o32s)
             t = timeit(lambda: _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=dq, workspace=ws, o32=o32s),
                        args.reps)
-            print(f"attn bwd tiled (attn_delta from o32 + dkdv + dq)  {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF")
+            print(f"attn bwd tiled (dq with delta from o32, dkdv)  {t:8.1f} us  {fl_b / t / 1e6:7.1f} TF")
 
 
 if __name__ == "__main__":

@@ -354,38 +354,18 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
   }
 }
 
-// delta[b,h,q] = sum_d dO . O  (fp32): 8 lanes per (row, head), one 16-B chunk each, so a wave instruction reads 8
-// whole 128-B head rows; fixed shuffle-tree order.  (One thread per (row, head) read 64 lines per instruction: 6x
-// off the HBM rate at T = 577.)
-// With the forward's fp32 O (o32) delta is exact to fp32: under the reference's x sqrt(hd) scaling most softmax rows are
-// saturated, where dS = P (dP - delta) is a tiny difference and delta from the bf16-rounded O swamps it (measured: the
-// Q / K weight gradients of a saturated head 10x off the bf16-rounding oracle).
+// dQ of 128 queries per workgroup (4 waves x 32) over 64-key tiles.  It runs before attn_bwd_dkdv_mfma and forms
+// delta[q] = sum_d dO . O for its own queries from the dO fragments it holds anyway and the forward's O (the fp32 copy
+// when there is one): each lane dots its 32 columns of the row, the two lane halves are added (fixed order); the
+// result is stored for the dK / dV kernel.  No separate delta pass re-reading dO (was attn_delta, 29 us per layer at
+// C5).  With the forward's fp32 O (o32) delta is exact to fp32: under the reference's x sqrt(hd) scaling most softmax
+// rows are saturated, where dS = P (dP - delta) is a tiny difference and delta from the bf16-rounded O swamps it
+// (measured: the Q / K weight gradients of a saturated head 10x off the bf16-rounding oracle).
 template <class TO>
-__global__ __launch_bounds__(256) void attn_delta(const TO* __restrict__ o, const bf16_t* __restrict__ d_o,
-                                                  float* __restrict__ delta, int64_t B, int64_t Tn, int64_t H) {
-  const int64_t total = B * Tn * H * 8;               // a multiple of 8: the 8 lanes of a row leave the loop together
-  const int64_t D = H * HD;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t u = t >> 3;
-    const int c = (int)(t & 7);
-    const int64_t row = u / H, h = u % H, b = row / Tn, q = row % Tn;
-    const s16x8 vg = *reinterpret_cast<const s16x8*>(d_o + row * D + h * HD + c * 8);
-    float va[8];
-    ld4<TO>(o + row * D + h * HD + c * 8, va);
-    ld4<TO>(o + row * D + h * HD + c * 8 + 4, va + 4);
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += va[j] * bf2f((bf16_t)vg[j]);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    if (c == 0) delta[(b * H + h) * Tn + q] = s;
-  }
-}
-
 __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ d_o,
-                                                        const float* __restrict__ lse, const float* __restrict__ delta,
-                                                        bf16_t* __restrict__ dqkv, int64_t Tn, int64_t H, float scale) {
+                                                        const TO* __restrict__ o, const float* __restrict__ lse,
+                                                        float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                        int64_t Tn, int64_t H, float scale) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hf = lane >> 5;
   int64_t blk, bh;
@@ -403,7 +383,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
     gf[s] = glb_frag(d_o + b * Tn * D, D, q0, Tn, h * HD, s, lane);
   }
   const float nls = q < Tn ? -lse[bh * Tn + q] / scale : 0.f;   // initial S accumulator (row constant)
-  const float ndl = q < Tn ? -delta[bh * Tn + q] : 0.f;          // initial dP accumulator
+  // O row pieces for delta: loaded with the first K / V tile (their wait is the tile's), summed after it
+  float va[4][8];
+  {
+    const TO* orow = o + (b * Tn + min(q, Tn - 1)) * D + h * HD + 8 * hf;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ld4<TO>(orow + 16 * s, va[s]);
+      ld4<TO>(orow + 16 * s + 4, va[s] + 4);
+    }
+  }
   f32x16 dq[2] = {f32x16{}, f32x16{}};
   const int ntiles = (int)((Tn + KT - 1) / KT);
   uint4 rk[2], rv[2];
@@ -411,6 +400,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
   tile_load(base, ld, 0, Tn, 2 * D + h * HD, tid, rv);
   tile_store(smem, tid, rk);
   tile_store(smem + TILE, tid, rv);
+  float dl = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += va[s][j] * (float)gf[s][j];
+  dl += __shfl_xor(dl, 32, 64);
+  if (hf == 0 && q < Tn) delta[bh * Tn + q] = dl;
+  const float ndl = q < Tn ? -dl : 0.f;                          // initial dP accumulator
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
@@ -1254,8 +1251,6 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
   VIT_REQUIRE(qkv && o && d_o && lse && dqkv && workspace && B > 0 && T > 0 && H > 0 && hd > 0,
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
-  const int64_t rows = B * T * H;
-  const unsigned dgrid = (unsigned)std::min<int64_t>((rows * 8 + 255) / 256, 16384);
   if (bwd_fused(B, T, H, hd, dtype)) {
     // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid; delta is
     // formed in the kernel from P and dP (o and o32 are not read)
@@ -1278,12 +1273,14 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
     }
 #undef BWD
   } else if (use_mfma(dtype, hd)) {
-    float* delta = (float*)workspace;
-    if (o32) attn_delta<float><<<dgrid, 256, 0, s>>>(o32, (const bf16_t*)d_o, delta, B, T, H);
-    else attn_delta<bf16_t><<<dgrid, 256, 0, s>>>((const bf16_t*)o, (const bf16_t*)d_o, delta, B, T, H);
+    float* delta = (float*)workspace;                  // written by the dQ kernel, read by the dK / dV kernel
     const unsigned grid = (unsigned)(((T + 127) / 128) * B * H);   // 1-D: xcd_block() maps it
-    attn_bwd_dq_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
-                                          scale);
+    if (o32)
+      attn_bwd_dq_mfma<float><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, o32, lse, delta,
+                                                   (bf16_t*)dqkv, T, H, scale);
+    else
+      attn_bwd_dq_mfma<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, (const bf16_t*)o, lse,
+                                                    delta, (bf16_t*)dqkv, T, H, scale);
     attn_bwd_dkdv_mfma<<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, delta, (bf16_t*)dqkv, T, H,
                                             scale);
   } else {
