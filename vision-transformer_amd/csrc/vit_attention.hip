@@ -191,6 +191,30 @@ VIT_DEV void tile_store(bf16_t* lds, int tid, const uint4 (&reg)[2]) {
   }
 }
 
+// The same 64-row tile by LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write): 8 pieces of 8 rows,
+// wave w of the 4 issues pieces 2w and 2w + 1, lane-linear destination with the chunk swizzle applied to the source
+// address (the layout tile_store writes; aswz(r) = aswz(r mod 64)).  Rows >= nrows are clamped to nrows - 1: finite
+// data, and every caller masks those rows (keys: S = -inf or dS = 0; queries: lse = +inf).  Issued as inline asm so
+// the compiler's waitcnt pass does not drain it at the LDS reads of the other buffer; the caller retires it with
+// tile_wait() before the barrier that publishes the buffer.
+VIT_DEV void tile_dma(const bf16_t* __restrict__ src, int64_t ld, int64_t r0, int64_t nrows, int64_t col0, bf16_t* img,
+                      int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pc = 2 * wave + i;
+    const int rl = pc * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ aswz(rl);
+    const bf16_t* g = src + min(r0 + rl, nrows - 1) * ld + col0 + c * 8;
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(img + pc * 512));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+#pragma clang diagnostic pop
+  }
+}
+VIT_DEV void tile_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // 32x32x16 operand fragment from a [row][64] tile, rows rb..rb+31, k-step s (d = 16s..16s+15):
 // lane holds X[rb + (lane&31)][16s + 8(lane>>5) + 0..7]
 VIT_DEV bf16x8_t row_frag(const bf16_t* t, int rb, int s, int lane) {
@@ -276,18 +300,17 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
   f32x16 oacc[2] = {f32x16{}, f32x16{}};
   float m_run = -INFINITY, l_run = 0.f;
   const int ntiles = (int)((Tn + KT - 1) / KT);
-  uint4 rk[2], rv[2];
-  tile_load(base, ld, 0, Tn, D + h * HD, tid, rk);
-  tile_load(base, ld, 0, Tn, 2 * D + h * HD, tid, rv);
-  tile_store(smem, tid, rk);
-  tile_store(smem + TILE, tid, rv);
+  tile_dma(base, ld, 0, Tn, D + h * HD, smem, wave, lane);
+  tile_dma(base, ld, 0, Tn, 2 * D + h * HD, smem + TILE, wave, lane);
+  tile_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < ntiles;
     if (more) {
-      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, D + h * HD, tid, rk);
-      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, 2 * D + h * HD, tid, rv);
+      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;       // read in iteration t - 1, released by its closing barrier
+      tile_dma(base, ld, (int64_t)(t + 1) * KT, Tn, D + h * HD, nb, wave, lane);
+      tile_dma(base, ld, (int64_t)(t + 1) * KT, Tn, 2 * D + h * HD, nb + TILE, wave, lane);
     }
     const bf16_t* Ks = smem + cur * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
@@ -328,11 +351,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
         oacc[db] = mfma32(tr_frag(Vs, kb + 16, db, lane), pb1, oacc[db]);
       }
     }
-    if (more) {
-      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;
-      tile_store(nb, tid, rk);
-      tile_store(nb + TILE, tid, rv);
-    }
+    tile_wait();
     __syncthreads();
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -361,8 +380,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
 // C5).  With the forward's fp32 O (o32) delta is exact to fp32: under the reference's x sqrt(hd) scaling most softmax
 // rows are saturated, where dS = P (dP - delta) is a tiny difference and delta from the bf16-rounded O swamps it
 // (measured: the Q / K weight gradients of a saturated head 10x off the bf16-rounding oracle).
+#ifndef ATT_DQ_MINB              // A/B builds only: workgroups per CU the dQ kernel's register budget is sized for
+#define ATT_DQ_MINB 2
+#endif
 template <class TO>
-__global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ d_o,
+__global__ __launch_bounds__(256, ATT_DQ_MINB) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ d_o,
                                                         const TO* __restrict__ o, const float* __restrict__ lse,
                                                         float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                         int64_t Tn, int64_t H, float scale) {
@@ -395,11 +417,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
   }
   f32x16 dq[2] = {f32x16{}, f32x16{}};
   const int ntiles = (int)((Tn + KT - 1) / KT);
-  uint4 rk[2], rv[2];
-  tile_load(base, ld, 0, Tn, D + h * HD, tid, rk);
-  tile_load(base, ld, 0, Tn, 2 * D + h * HD, tid, rv);
-  tile_store(smem, tid, rk);
-  tile_store(smem + TILE, tid, rv);
+  tile_dma(base, ld, 0, Tn, D + h * HD, smem, wave, lane);
+  tile_dma(base, ld, 0, Tn, 2 * D + h * HD, smem + TILE, wave, lane);
   float dl = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s)
@@ -408,13 +427,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
   dl += __shfl_xor(dl, 32, 64);
   if (hf == 0 && q < Tn) delta[bh * Tn + q] = dl;
   const float ndl = q < Tn ? -dl : 0.f;                          // initial dP accumulator
+  tile_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < ntiles;
     if (more) {
-      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, D + h * HD, tid, rk);
-      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, 2 * D + h * HD, tid, rv);
+      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;       // read in iteration t - 1, released by its closing barrier
+      tile_dma(base, ld, (int64_t)(t + 1) * KT, Tn, D + h * HD, nb, wave, lane);
+      tile_dma(base, ld, (int64_t)(t + 1) * KT, Tn, 2 * D + h * HD, nb + TILE, wave, lane);
     }
     const bf16_t* Ks = smem + cur * 2 * TILE;
     const bf16_t* Vs = Ks + TILE;
@@ -448,11 +469,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
         dq[db] = mfma32(tr_frag(Ks, kb + 16, db, lane), d1, dq[db]);
       }
     }
-    if (more) {
-      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;
-      tile_store(nb, tid, rk);
-      tile_store(nb + TILE, tid, rv);
-    }
+    tile_wait();
     __syncthreads();
   }
   if (q < Tn) {
@@ -469,7 +486,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv,
+#ifndef ATT_DKDV_MINB            // A/B builds only: workgroups per CU the dK / dV kernel is sized for
+#define ATT_DKDV_MINB 3
+#endif
+__global__ __launch_bounds__(256, ATT_DKDV_MINB) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv,
                                                           const bf16_t* __restrict__ d_o,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -494,7 +514,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   }
   f32x16 dk[2] = {f32x16{}, f32x16{}}, dv[2] = {f32x16{}, f32x16{}};
   const int ntiles = (int)((Tn + KT - 1) / KT);
-  uint4 rq[2], rg[2];
   float st_l = 0.f, st_d = 0.f;
   auto load_stats = [&](int t) {
     if (tid < KT) {
@@ -503,22 +522,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       st_d = qq < Tn ? -delta[bh * Tn + qq] : 0.f;
     }
   };
-  tile_load(base, ld, 0, Tn, h * HD, tid, rq);
-  tile_load(gbase, D, 0, Tn, h * HD, tid, rg);
+  tile_dma(base, ld, 0, Tn, h * HD, smem, wave, lane);
+  tile_dma(gbase, D, 0, Tn, h * HD, smem + TILE, wave, lane);
   load_stats(0);
-  tile_store(smem, tid, rq);
-  tile_store(smem + TILE, tid, rg);
   if (tid < KT) {
     stat[0][0][tid] = st_l;
     stat[0][1][tid] = st_d;
   }
+  tile_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < ntiles;
     if (more) {
-      tile_load(base, ld, (int64_t)(t + 1) * KT, Tn, h * HD, tid, rq);
-      tile_load(gbase, D, (int64_t)(t + 1) * KT, Tn, h * HD, tid, rg);
+      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;       // read in iteration t - 1, released by its closing barrier
+      tile_dma(base, ld, (int64_t)(t + 1) * KT, Tn, h * HD, nb, wave, lane);
+      tile_dma(gbase, D, (int64_t)(t + 1) * KT, Tn, h * HD, nb + TILE, wave, lane);
       load_stats(t + 1);
     }
     const bf16_t* Qs = smem + cur * 2 * TILE;
@@ -561,14 +580,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       }
     }
     if (more) {
-      bf16_t* nb = smem + (cur ^ 1) * 2 * TILE;
-      tile_store(nb, tid, rq);
-      tile_store(nb + TILE, tid, rg);
       if (tid < KT) {
         stat[cur ^ 1][0][tid] = st_l;
         stat[cur ^ 1][1][tid] = st_d;
       }
     }
+    tile_wait();
     __syncthreads();
   }
   const int64_t key = k0 + (lane & 31);
