@@ -357,6 +357,81 @@ def test_ddp_gradient_buckets_gloo(comm_dtype):
     assert sorted(res) == [(0, True), (1, True)]
 
 
+class _IndexedImages(torch.utils.data.Dataset):
+    """Synthetic images that record which indices were read (shard order per epoch)."""
+
+    def __init__(self, n):
+        import train as T
+        self.base = T.SyntheticImages(n, 3, 32, 4, seed=3)
+        self.seen = []
+
+    def __len__(self):
+        return len(self.base)
+
+    def __getitem__(self, i):
+        self.seen.append(int(i))
+        return self.base[i]
+
+
+class _SignClassifier(torch.nn.Module):
+    """Predicts (number of positive pixels) mod 4: a deterministic stand-in whose accuracy is known exactly."""
+
+    def forward(self, x):
+        k = (x > 0).flatten(1).sum(1) % 4
+        return torch.nn.functional.one_hot(k, 4).float()
+
+
+def _dp_train_worker(rank, world, port, q):
+    import torch.distributed as dist
+    import train as T
+    from VisionTransformer import config
+    from sklearn.metrics import accuracy_score
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    T.device = "cpu"
+    ds = _IndexedImages(16)
+    sampler = torch.utils.data.DistributedSampler(ds, seed=0)
+    dl = torch.utils.data.DataLoader(ds, batch_size=4, sampler=sampler, drop_last=True)
+    cfg = config.ViTConfig(3, 4, 4, 32, 16, 2, 1, "cpu", 4)
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        T.train(cfg, dl, None, 1, 1, os.path.join(tmp, "l"), os.path.join(tmp, "ck"))     # epochs 0 and 1
+    orders = [ds.seen[:8], ds.seen[8:16]]
+    # evaluate(): each rank scores its shard of the test set, the counts are all-reduced
+    ts = T.SyntheticImages(32, 3, 32, 4, seed=7)
+    tl = torch.utils.data.DataLoader(ts, batch_size=4, drop_last=True,
+                                     sampler=torch.utils.data.DistributedSampler(ts, shuffle=False))
+    acc = T.evaluate(_SignClassifier(), tl, accuracy_score)
+    full = torch.utils.data.DataLoader(ts, batch_size=32)
+    x, y = next(iter(full))
+    want = float((_SignClassifier()(x).argmax(-1) == y).float().mean())
+    q.put((rank, orders, acc, want))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_train_epochs_and_evaluate_gloo():
+    """2-rank gloo, host path: train() calls DistributedSampler.set_epoch every epoch,
+    so each rank's shard order differs between epochs and the two ranks' shards partition the set; evaluate() on a
+    sharded test loader returns the accuracy over the WHOLE test set on every rank (all-reduced counts)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (r0, o0, a0, w0), (r1, o1, a1, w1) = res
+    for e in range(2):
+        assert sorted(o0[e] + o1[e]) == list(range(16)), e       # the shards partition the set every epoch
+    assert o0[0] != o0[1] and o1[0] != o1[1]                      # set_epoch: a new order each epoch
+    assert abs(a0 - w0) < 1e-12 and abs(a1 - w1) < 1e-12 and 0.0 < w0 < 1.0
+
+
 def test_attention_probs_warns_once_after_fused_forward():
     """The fused forward keeps attention probabilities only with store_attention_probs=True; reading them after a
     forward that skipped them returns None (as before) but warns once, pointing at the flag."""

@@ -329,6 +329,34 @@ def test_parameter_hooks_with_gradient_accumulation():
             assert torch.allclose(p.grad, plain[k].grad, rtol=1e-6, atol=1e-7), k
 
 
+@pytest.mark.parametrize("hook", [True, False])
+def test_freeze_between_accumulating_backwards(hook):
+    """a parameter frozen between two accumulating backwards keeps the .grad it had (autograd never touches
+    a frozen parameter's gradient), also when it shares the fused QKV gradient region with heads that still train
+    and when another parameter's `register_hook` sends the backward through the hook-accumulation path."""
+    ocfg = _hd64_cfg()
+    st = O.init_state(ocfg, seed=15)
+    x, y = O.synthetic_batch(ocfg)
+    x, y = x.to(DEV), y.to(DEV)
+    m = _model(ocfg, st).eval()
+    if hook:
+        m.mlp[3].weight.register_hook(lambda g: g * 0.5)
+    frozen_keys = ["transformer_encoder.blocks.0.multi_head.heads.0.query.weight",   # shares block 0's QKV region
+                   "transformer_encoder.blocks.1.ffwd.mlp.0.weight"]                    # a region of its own
+    named = dict(m.named_parameters())
+    cross_entropy(m(x), y).backward()
+    first = {k: p.grad.clone() for k, p in named.items()}
+    for k in frozen_keys:
+        named[k].requires_grad_(False)
+    cross_entropy(m(x), y).backward()
+    for k in frozen_keys:
+        assert torch.equal(named[k].grad, first[k]), k
+    # the parameters that still train accumulated g1 + g2 = 2 g1 (same input, eval mode)
+    for k in ("transformer_encoder.blocks.0.multi_head.heads.0.key.weight", "mlp.3.weight",
+              "transformer_encoder.blocks.1.ffwd.mlp.2.weight"):
+        assert torch.allclose(named[k].grad, 2 * first[k], rtol=1e-6, atol=1e-7), k
+
+
 def test_deepcopy_snapshot_is_independent():
     """A deep copy (EMA / best-model snapshot) builds its own engine: same outputs, and training the original does
     not touch the copy."""
@@ -416,6 +444,29 @@ def test_fused_adamw_reload_state_matches_torch():
     steps = sorted({float(opt.state[p]["step"]) for p in m.parameters()})
     assert steps == [float(ref.state[shadow[0]]["step"])] == [3.0]
     torch.optim.AdamW(shadow, lr=1e-3).load_state_dict(opt.state_dict())
+
+
+def test_fused_adamw_follows_repointed_storage():
+    """`p.data = new` on a parameter no engine owns, and a replaced moment tensor, after the chunk table was
+    cached: the next steps update the new storage (as torch.optim.AdamW does), not the old one."""
+    torch.manual_seed(0)
+    ps = [torch.randn(37, 5, device=DEV).requires_grad_(True), torch.randn(300, device=DEV).requires_grad_(True)]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    opt = FusedAdamW(ps, lr=1e-2, weight_decay=1e-2)
+    ropt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=1e-2)
+    for i in range(4):
+        grads = [torch.randn_like(p) for p in ps]
+        for p, r, g in zip(ps, ref, grads):
+            p.grad, r.grad = g.clone(), g.clone()
+        if i == 2:
+            with torch.no_grad():
+                ps[0].data = ps[0].data.clone() + 1.0       # new storage
+                ref[0].data = ref[0].data.clone() + 1.0
+                opt.state[ps[1]]["exp_avg"] = opt.state[ps[1]]["exp_avg"].clone()
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, ref):
+        assert (p.detach() - r.detach()).abs().max().item() < 1e-6
 
 
 def test_missing_library_fails_loudly(monkeypatch):

@@ -578,6 +578,12 @@ class Engine:
             self._acc_old = self.G.clone()
             beta = 0.0
         req = {k: any(p.requires_grad for p in ps) for k, ps in self.owners.items()}
+        # a frozen per-head parameter whose .grad is still a view of G shares the fused QKV gradient region with the
+        # heads that do train; that region is rewritten as a whole, so keep the frozen view's value aside (autograd
+        # leaves a frozen parameter's .grad untouched)
+        self._frozen_keep = [(gv, gv.clone()) for p, gv in self.grad_views
+                             if not p.requires_grad and p.grad is not None and p.grad.data_ptr() == gv.data_ptr()
+                             and self._acc_old is None]
         # the backward stops at the first block below which nothing (parameters, input image) needs a gradient
         below = tape.x_grad or any(req[k] for k in ("conv_w", "conv_b", "cls", "pos"))
         need_from = {}
@@ -678,6 +684,11 @@ class Engine:
                 dxm_full = torch.zeros(M, D, dtype=dt, device=dev)
                 _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
                 do, dx_mid = do_full, dxm_full
+            if o32 is None and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
+                # the forward chose the fused backward (no fp32 O kept) and a library option changed since: the tiled
+                # backward would form delta from the bf16 O, inexact under saturated softmax
+                raise RuntimeError("attention backward needs the fp32 O that this forward did not keep: the "
+                                   "attn_bwd_split library option changed between forward and backward")
             # bytes: qkv, dO, dqkv (+ O and o32 for the tiled backward's delta pass)
             mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 7 * M * D * es + 4 * B * H * T + (M * D * es + 4 * M * D if o32
                                                                                           is not None else 0))
@@ -741,6 +752,9 @@ class Engine:
         (backward() set `_acc_old`): the hooks see the increment, then the previous gradients are added back."""
         old = getattr(self, "_acc_old", None)
         self._acc_old = None
+        for gv, keep in getattr(self, "_frozen_keep", None) or ():
+            gv.copy_(keep)
+        self._frozen_keep = None
         for p, gv in self.grad_views:
             if not p.requires_grad or p.grad is None:
                 continue
@@ -754,7 +768,15 @@ class Engine:
                 if g is not p.grad:
                     p.grad.copy_(g)
         if old is not None:
-            self.G.add_(old)
+            # the previous gradients go back under the views of the parameters this backward produced a gradient
+            # for; every other view (frozen meanwhile, or in a region no kernel rewrote) gets its old value back,
+            # never old + old
+            for p, gv in self.grad_views:
+                ov = torch.as_strided(old, gv.shape, gv.stride(), gv.storage_offset())
+                if p.requires_grad and p.grad is not None and p.grad.data_ptr() == gv.data_ptr():
+                    gv.add_(ov)
+                else:
+                    gv.copy_(ov)
         for p, gv in self.grad_views:
             if not p.requires_grad or p.grad is None:
                 continue

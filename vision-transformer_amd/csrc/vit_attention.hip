@@ -668,14 +668,25 @@ VIT_DEV void dma_head_slice(__amdgpu_buffer_rsrc_t rs, int64_t row0, int64_t ld,
 }
 
 // Row-contiguous store of a [rows][64] bf16 LDS image (row stride RS elements, no swizzle) to global rows (row stride
-// ld): 8 lanes per 128-B row.
+// ld): 8 lanes per 128-B row.  Rows of a stride that is not a multiple of 8 elements (the padded dQ staging, 68) are
+// only 8-B aligned, so the 16-B piece is read as two 8-B LDS reads there.
 template <int RS>
 VIT_DEV void store_rows64(const bf16_t* img, int rows, int valid_rows, bf16_t* dst, int64_t ld, int tid,
                           int nthreads) {
+  static_assert(RS % 4 == 0, "store_rows64: rows must be 8-B aligned");
   for (int q = tid; q < rows * 8; q += nthreads) {
     const int r = q >> 3, c = q & 7;
-    if (r < valid_rows)
-      *reinterpret_cast<uint4*>(dst + (int64_t)r * ld + c * 8) = *reinterpret_cast<const uint4*>(img + r * RS + c * 8);
+    if (r < valid_rows) {
+      uint4 v;
+      if (RS % 8 == 0) {
+        v = *reinterpret_cast<const uint4*>(img + r * RS + c * 8);
+      } else {
+        const uint2 lo = *reinterpret_cast<const uint2*>(img + r * RS + c * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(img + r * RS + c * 8 + 4);
+        v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+      *reinterpret_cast<uint4*>(dst + (int64_t)r * ld + c * 8) = v;
+    }
   }
 }
 

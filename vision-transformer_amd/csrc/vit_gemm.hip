@@ -651,6 +651,7 @@ VIT_DEV void dma_offsets4g(int64_t ld, int64_t rows, int64_t r0, int64_t k0, int
 VIT_DEV void dma_half_g(const char* base, const uint32_t (&off)[2], uint32_t soff, bf16_t* half, int wave) {
   const uint32_t lds = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(half + wave * 2 * 512));
+  const uint32_t lds1 = lds + 0x400;                  // second piece's LDS base (s_mov only: SCC stays untouched)
   const char* p0 = base + off[0] + soff;
   const char* p1 = base + off[1] + soff;
 #pragma clang diagnostic push
@@ -659,9 +660,9 @@ VIT_DEV void dma_half_g(const char* base, const uint32_t (&off)[2], uint32_t sof
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %0, off\n\t"
-      "s_add_u32 m0, %2, 0x400\n\t"
+      "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off" ::"v"(p0), "v"(p1), "s"(lds)
+      "global_load_lds_dwordx4 %1, off" ::"v"(p0), "v"(p1), "s"(lds), "s"(lds1)
       : "memory", "m0");
 #pragma clang diagnostic pop
 }

@@ -57,7 +57,11 @@ def _writer(log_dir):
 
 @torch.no_grad()
 def evaluate(model, test_loader, eval_func, avg=None):
-    """Mean over batches of eval_func(labels, argmax(logits)) (train.py:29-44)."""
+    """Mean over batches of eval_func(labels, argmax(logits)) (train.py:29-44).
+
+    Under data parallelism (an initialized process group of world size > 1) every rank scores the batches of its
+    own shard of the test set and the (score sum, batch count) pair is all-reduced, so every rank returns the mean
+    over all ranks' batches — with equal batches (drop_last), the accuracy over the whole test set."""
     model.eval()
     score = 0.0
     n = 0
@@ -71,7 +75,27 @@ def evaluate(model, test_loader, eval_func, avg=None):
             score += eval_func(labels, predictions, average=avg, zero_division=0.0)
         n += 1
     model.train()
+    _, world = _rank_world()
+    if world > 1:
+        on_dev = dist.get_backend() == "nccl"
+        t = torch.tensor([float(score), float(n)], dtype=torch.float64,
+                         device=torch.device("cuda", torch.cuda.current_device()) if on_dev else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        score, n = float(t[0]), int(t[1])
     return score / max(n, 1)
+
+
+def _set_epoch(loader, epoch):
+    """DistributedSampler.set_epoch on the loader's sampler (also behind data.DeviceBatches), so each epoch draws a
+    new shard order on every rank."""
+    for obj in (loader, getattr(loader, "loader", None)):
+        if obj is None:
+            continue
+        for s in (getattr(obj, "sampler", None), getattr(getattr(obj, "batch_sampler", None), "sampler", None)):
+            if isinstance(s, torch.utils.data.DistributedSampler):
+                s.set_epoch(epoch)
+                return True
+    return False
 
 
 def search_checkpoint(dir):
@@ -108,11 +132,14 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
           log_every=1, max_steps=None, reference_loop=False):
     """The reference training loop (train.py:60-119) on the HIP path.  Returns the last epoch's summed loss.
 
-    Defaults keep the GPU busy: the epoch loss is summed on the device, validation runs every `eval_iter` epochs and a
-    resumed run continues its step counter.  `reference_loop=True` restores the reference's bookkeeping exactly:
-    validation after every epoch (its eval_iter gate is commented out, train.py:114), `iteration` restarting at 0 on
-    resume (train.py:67; the checkpoint's `step` is not read back) and the epoch loss as the host sum of each step's
-    loss.item() (train.py:97-99: one host sync per step)."""
+    Defaults keep the GPU busy: no host sync inside the epoch — the epoch loss is summed on the device and the per-step
+    "Loss/train_batch" scalars (every `log_every` steps, train.py:98) stay on the device until the epoch ends, when they
+    are written in one transfer; validation runs every `eval_iter` epochs and a resumed run continues its step counter.
+    `reference_loop=True` restores the reference's bookkeeping exactly: validation after every epoch (its eval_iter
+    gate is commented out, train.py:114), `iteration` restarting at 0 on resume (train.py:67; the checkpoint's `step`
+    is not read back) and the epoch loss as the host sum of each step's loss.item() (train.py:97-99: one host sync
+    per step).  Under data parallelism a DistributedSampler gets `set_epoch(epoch)` every epoch and `evaluate`
+    all-reduces its counts."""
     rank, world = _rank_world()
     saved_epoch = search_checkpoint(checkpoint_dir)
     torch.manual_seed(0)                              # identical init on every rank
@@ -139,8 +166,10 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
     writer = _writer(log_dir) if rank == 0 else None
     running_loss = 0.0
     for epoch in range(saved_epoch, epochs + 1):
+        _set_epoch(train_loader, epoch)
         loss_sum = torch.zeros((), device=device)
         host_loss = 0.0
+        logged = []                                   # (iteration, device loss) written at the epoch's end
         t0 = time.time()
         nb = 0
         for tensors, labels in train_loader:
@@ -153,14 +182,19 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
             optimizer.step()
             if reference_loop:
                 host_loss += loss.item()
+                if writer is not None:
+                    writer.add_scalar("Loss/train_batch", loss.item(), iteration)
             else:
                 loss_sum += loss.detach()
-            if writer is not None and log_every and iteration % log_every == 0:
-                writer.add_scalar("Loss/train_batch", loss.item(), iteration)
+                if writer is not None and log_every and iteration % log_every == 0:
+                    logged.append((iteration, loss.detach()))
             iteration += 1
             nb += 1
             if max_steps and nb >= max_steps:
                 break
+        if logged:
+            for (it, _), v in zip(logged, torch.stack([v for _, v in logged]).tolist()):
+                writer.add_scalar("Loss/train_batch", v, it)
         running_loss = host_loss if reference_loop else float(loss_sum.item())
         dt = time.time() - t0
         acc = None
@@ -281,13 +315,15 @@ def main():
             train_set = D.SyntheticRawImages(args.train_size, (32, 32, 3), args.classes, seed=1 + rank)
             test_set = D.SyntheticRawImages(args.test_size, (32, 32, 3), args.classes, seed=10_000)
     sampler = torch.utils.data.DistributedSampler(train_set) if world > 1 else None
+    # the test set is sharded too; evaluate() all-reduces the counts
+    tsampler = torch.utils.data.DistributedSampler(test_set, shuffle=False) if world > 1 else None
     if args.data != "synthetic" and device == "cuda":
         from VisionTransformer import data as D
         # one transform (and coefficient workspace) per loader: each stages its batches on its own side stream
         train_loader = D.DeviceBatches(D.raw_loader(train_set, args.batch, shuffle=True, num_workers=args.workers,
                                                     sampler=sampler), D.GpuImageTransform(args.img), device)
-        test_loader = D.DeviceBatches(D.raw_loader(test_set, args.batch, shuffle=False, num_workers=args.workers),
-                                      D.GpuImageTransform(args.img), device)
+        test_loader = D.DeviceBatches(D.raw_loader(test_set, args.batch, shuffle=False, num_workers=args.workers,
+                                                   sampler=tsampler), D.GpuImageTransform(args.img), device)
     else:
         if args.data != "synthetic":
             from VisionTransformer import data as D
@@ -296,7 +332,7 @@ def main():
                                                    sampler=sampler, num_workers=args.workers, drop_last=True,
                                                    pin_memory=pin)
         test_loader = torch.utils.data.DataLoader(test_set, batch_size=args.batch, num_workers=args.workers,
-                                                  drop_last=True, pin_memory=pin)
+                                                  sampler=tsampler, drop_last=True, pin_memory=pin)
     train(cfg, train_loader, test_loader, args.epochs, args.eval_iter, args.log_dir, args.checkpoint_dir,
           lr=args.lr, max_steps=args.steps, reference_loop=args.reference_loop)
     if world > 1:
