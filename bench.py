@@ -386,10 +386,7 @@ def run(args, rank, world, local):
                     "ms_per_step": d["ms_per_step"], "launches_per_step": d["launches_per_step"],
                     "events_over": "every hot launch of the last of the timed steps (HIP events on the compute stream)",
                     "avg_launch_us": d["avg_launch_us"],
-                    "kernels": {"gemm_wgrad": "gemm_bf16_v4<false,false,float,EPI_SLAB> + splitk_reduce",
-                                "gemm_fwd": "gemm_bf16_v4<true,true,bf16,*>", "gemm_dgrad": "gemm_bf16_v4<true,false,*>",
-                                "attn_fwd": "attn_fwd_fused / attn_fwd_mfma", "attn_bwd": "attn_bwd_fused / tiled",
-                                "ln_fwd": "ln_fwd_kernel", "ln_bwd": "ln_bwd_kernel"}.get(dom, dom)}
+                    "kernels": family_kernels(dom)}
                 for f, v in fams.items():
                     pk_f = peak if (f.startswith("gemm") or f.startswith("attn")) else None
                     v["mfma_frac"] = round(v["tflops"] * 1e12 / peak, 4) if pk_f else None
@@ -404,6 +401,21 @@ def run(args, rank, world, local):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def family_kernels(fam):
+    """The kernels a roofline family's HIP events time (what `roofline.kernels` names): every launch between the
+    engine's family marks, the split-K pieces included."""
+    main = "gemm_bf16_v4"
+    slab = "gemm_bf16_v4<*,*,float,EPI_SLAB> + splitk_reduce"
+    return {"gemm_wgrad": f"gemm_bf16_v4<false,false,float,EPI_SLAB> + splitk_reduce<float>",
+            "gemm_fwd": f"{main}<true,true,bf16,*> (patch embedding: gemm_bf16_v4 EPI_PATCH) + the N=768 / K>=2304 "
+                        f"split-K tail and the pruned last block's split-K launches: {slab}",
+            "gemm_dgrad": f"{main}<true,false,*> + the split-K tail and the pruned last block's split-K launches: "
+                          f"{slab}",
+            "attn_fwd": "attn_fwd_fused / attn_fwd_mfma", "attn_bwd": "attn_bwd_fused / attn_bwd_dq_mfma + "
+                                                                      "attn_bwd_dkdv_mfma",
+            "ln_fwd": "ln_fwd16_kernel / ln_fwd_kernel", "ln_bwd": "ln_bwd_kernel"}.get(fam, fam)
 
 
 def _spawned(rank, args, world, port):

@@ -63,8 +63,8 @@ def test_base_width_bf16_engine_vs_oracle(train, preset, img):
     the oracle with fp32 arithmetic between them, the same with fp64, and the same with the MFMA flash-attention
     kernels' internal roundings (oracle `flash=True`: P and dS in bf16).  Gates:
       * logits within 1e-2 (norm-wise) of the bf16 oracle;
-      * every gradient except the attention query / key projections: error vs the fp32 oracle <= max(3e-2, 2 x the
-        largest error of a valid evaluation);
+      * every gradient except the attention query / key projections: error vs the fp32 oracle <= max(1e-2, 2 x the
+        largest error of a valid evaluation) — north_star's 1e-2 bf16 tolerance as the floor;
       * query / key projection gradients, per block with all heads concatenated: the same gate.  Per head they are
         chaotic under the saturating x sqrt(hd) softmax — block 1's attention gets gradient on query 0 only (the
         classifier reads token 0), and two valid evaluations differ by 10-200% on single heads (measured);
@@ -106,7 +106,7 @@ def test_base_width_bf16_engine_vs_oracle(train, preset, img):
         e_ours = err(ours, keys)
         e_ora = max(err(v, keys) for v in valid)
         worst.append((e_ours / max(e_ora, 1e-9), name, e_ours, e_ora))
-        if e_ours > max(1e-2 if name == "ALL" else 3e-2, 2 * e_ora):
+        if e_ours > max(1e-2, 2 * e_ora):
             bad.append((name, e_ours, e_ora))
     print("worst error ratios:", sorted(worst)[-4:])
     assert not bad, bad
@@ -481,17 +481,11 @@ def test_missing_library_fails_loudly(monkeypatch):
         m(x.to(DEV))
 
 
-def test_c2_full_shape_bf16_train_vs_oracle():
-    """BASELINE config 2 at its real shape: ViT-B/16 224^2, B=256 (M = 50,432 token rows), bf16, TRAIN mode (dropout),
-    two blocks (block 0 runs every GEMM at full M with dense gradients; block 1 is the pruned last block), through the
-    engine, against the oracle evaluated on the GPU with torch ops.  This brings the full-size kernels under parity
-    test: the K = 50,432 split-K weight-gradient GEMMs, the persistent many-round forward / dgrad GEMMs (591-2,364
-    tiles) and their split-K tails, the 3,072-item persistent attention backward.  Gates of
-    test_base_width_bf16_engine_vs_oracle: logits 1e-2; each gradient <= max(3e-2, 2 x the spread of valid bf16
-    evaluations: fp32 / fp64 / flash rounding between the same storage points); q/k per block; the whole vector
-    <= max(1e-2, 2 x spread)."""
-    ocfg = O.make_config("base", img=224, batch=256, blocks=2, num_classes=1000)
-    st = O.init_state(ocfg, seed=23)
+def _engine_vs_oracle_on_gpu(ocfg, seed):
+    """bf16 TRAIN-mode engine run vs the oracle evaluated on the GPU with torch ops, gated by the spread of valid bf16
+    evaluations (fp32 / fp64 / flash rounding between the same storage points): logits 1e-2; each gradient (q/k per
+    block, all heads together) <= max(1e-2, 2 x spread); the whole vector likewise."""
+    st = O.init_state(ocfg, seed=seed)
     m = _model(ocfg, st, torch.bfloat16).train()
     x, y = O.synthetic_batch(ocfg)
     xd, yd = x.to(DEV), y.to(DEV)
@@ -529,7 +523,22 @@ def test_c2_full_shape_bf16_train_vs_oracle():
         e_ours = err(ours, keys)
         e_ora = max(err(v, keys) for v in valid)
         worst.append((e_ours / max(e_ora, 1e-9), name, e_ours, e_ora))
-        if e_ours > max(1e-2 if name == "ALL" else 3e-2, 2 * e_ora):
+        if e_ours > max(1e-2, 2 * e_ora):
             bad.append((name, e_ours, e_ora))
     print("worst error ratios:", sorted(worst)[-4:])
     assert not bad, bad
+
+
+def test_c2_full_shape_bf16_train_vs_oracle():
+    """BASELINE config 2 at its real shape: ViT-B/16 224^2, B=256 (M = 50,432 token rows), bf16, TRAIN mode (dropout),
+    two blocks (block 0 runs every GEMM at full M with dense gradients; block 1 is the pruned last block), through the
+    engine, against the oracle evaluated on the GPU with torch ops.  This brings the full-size kernels under parity
+    test: the K = 50,432 split-K weight-gradient GEMMs, the persistent many-round forward / dgrad GEMMs (591-2,364
+    tiles) and their split-K tails, the 3,072-item persistent attention backward.  Gates of _engine_vs_oracle_on_gpu."""
+    _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=256, blocks=2, num_classes=1000), seed=23)
+
+
+def test_vit_base_full_depth_bf16_train_vs_oracle():
+    """ViT-B/16 at FULL depth (12 blocks, transformer.py:82-90), 224^2, B=8, bf16, train mode, through the engine vs the
+    oracle on the GPU (VERDICT r3 #4): the 12-block bf16 path under the same spread gates as the 2-block tests."""
+    _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=8, blocks=12, num_classes=1000), seed=29)

@@ -40,10 +40,10 @@ def test_gemm_bf16_exact_integers(akc, bkc, M, N, K):
     assert torch.equal(C.double(), ref), (C.double() - ref).abs().max()
 
 
-@pytest.mark.parametrize("impl", ["2", "4", "5"])
+@pytest.mark.parametrize("impl", ["2", "4"])
 @pytest.mark.parametrize("akc,bkc", LAYOUTS)
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (520, 264, 640), (1000, 776, 128), (72, 520, 192),
-                                   (2048, 768, 768), (304, 136, 32)])
+                                   (2048, 768, 768)])
 def test_gemm_bf16_kernels_exact(libopt, impl, akc, bkc, M, N, K):
     """Every LDS-DMA kernel variant (option gemm_impl) on ragged M/N tails and 1..12 k-tiles, exact on integers."""
     libopt("gemm_impl", int(impl))
@@ -428,50 +428,6 @@ def test_gemm_persistent_matches_one_per_item(libopt, variant):
             assert torch.equal(m1, m0)
     if variant in ("plain", "grouped"):
         assert torch.equal(c1, (a.double() @ b.double().t()).float().bfloat16())
-
-
-@pytest.mark.parametrize("variant", ["plain", "plain_cs", "plain_rs", "bias", "bias_relu_mask", "bias_drop_res",
-                                     "bias_drop_res_mask", "aux_cs", "auxm_cs", "auxm"])
-@pytest.mark.parametrize("M,N,K", [(23 * 256 + 100, 3072, 256), (3000, 776, 64), (1000, 392, 32), (4100, 768, 768)])
-def test_gemm_v5_matches_v4(libopt, variant, M, N, K):
-    """The two-group kernel (option gemm_impl 5: 256x128 group tiles, one group's epilogue beside the other's k-loop)
-    against v4 on integer data: outputs, mask4 bits and fused column sums bit for bit, on ragged M / N, several tiles
-    per group, and k-loops of 1, 2, 8 and 24 k-tiles of 32 (the DMA-pipeline edge cases)."""
-    g = torch.Generator().manual_seed(M + N + K)
-    a = _ints((M, K), gen=g)
-    b = _ints((N, K), gen=g)
-    bias = _ints((N,), gen=g, dtype=torch.float32)
-    aux = _ints((M, N), gen=g)
-    res = _ints((M, N), gen=g)
-    mask_in = torch.randint(0, 256, (_ops.mask4_bytes(M, N),), generator=g, dtype=torch.uint8).to(DEV)
-    ws = torch.empty(64 << 20, dtype=torch.float32, device=DEV)
-    results = []
-    for impl in (4, 5):
-        libopt("gemm_impl", impl)
-        libopt("gemm_tail", 0)
-        c = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        part = torch.full((_ops.colsum_part_rows(M), N), 7.0, device=DEV)
-        mask = torch.full((_ops.mask4_bytes(M, N),), 0xAA, dtype=torch.uint8, device=DEV)
-        if variant in ("aux_cs", "auxm_cs", "auxm", "plain_rs"):      # dgrad layout (B row-strided)
-            bt = b.t().contiguous()
-            kw = {"aux_cs": dict(aux=aux, ldaux=N, colsum_part=part), "auxm_cs": dict(aux=mask_in, colsum_part=part),
-                  "auxm": dict(aux=mask_in), "plain_rs": {}}[variant]
-            _ops.gemm(a, bt, c, M, N, K, K, N, N, b_kcontig=False, alpha=0.5, workspace=ws, **kw)
-        else:
-            kw = {"plain": {}, "plain_cs": dict(colsum_part=part), "bias": dict(bias=bias),
-                  "bias_relu_mask": dict(bias=bias, act=_ops.ACT_RELU, mask_out=mask),
-                  "bias_drop_res": dict(bias=bias, dropout_p=0.2, seed=5, res=res, ldres=N),
-                  "bias_drop_res_mask": dict(bias=bias, dropout_p=0.2, seed=5, res=res, ldres=N, mask_out=mask)}[variant]
-            _ops.gemm(a, b, c, M, N, K, K, K, N, workspace=ws, **kw)
-        results.append((c, part, mask))
-    (c4, p4, m4), (c5, p5, m5) = results
-    assert torch.equal(c5, c4)
-    if "cs" in variant:
-        assert torch.equal(p5, p4)
-    if "mask" in variant:
-        assert torch.equal(m5, m4)
-    if variant == "plain":
-        assert torch.equal(c5, (a.double() @ b.double().t()).float().bfloat16())
 
 
 def _attn_ref(qkv, B, T, H, hd, scale):

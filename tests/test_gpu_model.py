@@ -82,7 +82,7 @@ def test_hd64_fp32_vs_oracle(train):
 def test_bf16_vs_oracle_same_rounding(hd_heads):
     """bf16 compute (MFMA GEMM + MFMA attention when hd=64).  Gate: logits within 1e-2 (norm-wise) of the oracle
     that rounds to bf16 at the same storage points; every gradient's error against the fp32 oracle no worse than
-    max(3e-2, 2x) the bf16-emulating oracle's own error (K-projection gradients under the saturated x sqrt(hd)
+    max(1e-2, 2x) the bf16-emulating oracle's own error (K-projection gradients under the saturated x sqrt(hd)
     softmax are small differences of near-equal terms, so bf16 alone costs them ~10-20%)."""
     hd, H = hd_heads
     ocfg = O.make_config("micro", img=64, batch=4, blocks=2)
@@ -102,7 +102,7 @@ def test_bf16_vs_oracle_same_rounding(hd_heads):
     for k, p in m.named_parameters():
         ours, ora = _rel(p.grad.cpu(), g_32[k]), _rel(g_bf[k], g_32[k])
         worst.append((ours / max(ora, 1e-9), k, ours, ora))
-        assert ours <= max(3e-2, 2 * ora), (k, ours, ora)
+        assert ours <= max(1e-2, 2 * ora), (k, ours, ora)
     print("bf16 worst grad error ratios:", sorted(worst)[-3:])
 
 
@@ -338,16 +338,30 @@ def test_long_sequence_384_vs_oracle(dtype):
     assert _rel(logits.detach().cpu(), lg_bf) < 1e-2
     # The query / key projection gradients are dS-driven (dQ = dS K, dK = dS^T Q over 577 tokens, each softmax row
     # of dS summing to zero), so bf16 rounding of P / dS is amplified by cancellation (the bf16-emulating oracle
-    # itself is 4-12% off fp32 there).  The tiled T > 256 kernels do not round at exactly the storage points the
-    # oracle emulates (measured: 2.5-2.8x its error on one head, below it on the other), so the query / key gate is
-    # 4x the oracle's own bf16 error; every other tensor keeps the standard gate.  fp32 (above) pins the algorithm.
+    # itself is 4-12% off fp32 there).  Gate: the spread of VALID bf16 evaluations between the same
+    # storage points — fp32 and fp64 arithmetic, and the flash kernels' own roundings (oracle flash=True: P rounded
+    # for dV, dS rounded for dQ / dK, delta from the unrounded O, which is what the tiled kernels take from o32) —
+    # at 2x, floor 1e-2; query / key gradients per block with both heads together, as in the headline-width tests.
+    valid = [g_bf, O.loss_and_grads(st, x, y, ocfg, bf16=True, dtype=torch.float64)[2],
+             O.loss_and_grads(st, x, y, ocfg, bf16=True, flash=True)[2]]
+    groups = {}
+    for k in g_32:
+        if ".query." in k or ".key." in k:
+            groups.setdefault(k.split(".multi_head")[0] + " q/k (all heads)", []).append(k)
+        else:
+            groups[k] = [k]
+    ours = {k: p.grad.cpu() for k, p in m.named_parameters()}
+
+    def cat(gd, keys):
+        return torch.cat([gd[k].reshape(-1).double() for k in keys])
+
     bad = []
-    for k, p in m.named_parameters():
-        ours, ora = _rel(p.grad.cpu(), g_32[k]), _rel(g_bf[k], g_32[k])
-        gate = max(3e-2, (4 if (".key." in k or ".query." in k) else 2) * ora)
-        print(f"{k}: ours {ours:.4f} oracle-bf16 {ora:.4f}")
-        if ours > gate:
-            bad.append((k, ours, ora))
+    for name, keys in groups.items():
+        e = _rel(cat(ours, keys), cat(g_32, keys))
+        spread = max(_rel(cat(v, keys), cat(g_32, keys)) for v in valid)
+        print(f"{name}: ours {e:.4f} valid spread {spread:.4f} ratio {e / max(spread, 1e-9):.2f}")
+        if e > max(1e-2, 2 * spread):
+            bad.append((name, e, spread))
     assert not bad, bad
 
 

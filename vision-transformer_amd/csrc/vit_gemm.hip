@@ -1386,367 +1386,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// bf16 MFMA kernel v5: the epilogue of one tile runs beside another tile's k-loop.
-//
-//   In v4 the 8 waves of a CU share one 256x256 tile, so its epilogue (16-B row stores of 128 KiB, bias / dropout /
-//   residual / mask math) leaves the matrix pipes idle: 15-24 % of the forward and input-gradient GEMM time
-//   (profiles/r3b_gemm_ablation_ring_epilogue.log).  Here the workgroup is two independent wave GROUPS of 4 waves
-//   (group g = waves 4g..4g+3, one wave per SIMD, so every SIMD hosts one wave of each group), each with its own
-//   256x128 tile stream and its own LDS ring.  Group 1 runs half a tile period behind group 0: while one group runs
-//   its epilogue, the other group's k-loop owns the SIMDs' matrix pipes, and the stores drain in the background.
-//
-//   The workgroup's one s_barrier paces both groups: time is cut into INTERVALS of exactly one barrier each.  A group
-//   spends an interval on one 32-deep k-tile (32 MFMA 16x16x32 per wave), or one epilogue chunk, or nothing; both
-//   groups' schedules are known to every wave (static item lists), so the barrier counts always match.
-//     k-tile t (slot t % 3 of the group's 3-slot ring, 24 KiB: A [256][32], B [128][32] or [32][128]):
-//       [MFMA x 0..3 of t; fragments x 4..7 of t read first] vmcnt(k-tile t+1 landed) s_barrier
-//       [DMA of k-tile t+3 into slot t % 3; MFMA x 4..7 of t; fragments of t+1 read as their registers free]
-//     epilogue chunks (V5_E = 9 per tile): 0 issue the row-operand loads (residual / mask) and bias | 1 - | 2-5 four
-//       16-row x 32-column pieces each: math, 16-B stores, mask4 dwords, column sums | 5 column-sum partials -> LDS |
-//       6 column sums combined and stored, the NEXT tile's k-tiles 0-2 DMA'd (after every store, so the count wait
-//       of chunk 8 is exact) | 7 - | 8 k-tile 0 landed, barrier, its first fragments read.
-//   The next tile's DMA is issued behind the stores, so the k-loop's vmcnt waits only ever count DMA pieces.
-//   Group tile 256x128 moves 1.5x the LDS-DMA bytes per FLOP of v4's 256x256 (24 KiB per 32-deep k-tile and group).
-//   Every output element is the same MFMA sum in the same k order as v4 (bitwise equal C); column sums are added in
-//   a different row grouping (deterministic, within fp32 rounding of v4's).
-// ------------------------------------------------------------------------------------------------------------
-// timing ablations only (wrong results): no k-loop DMA / no k-loop barrier / no epilogue pieces
-#ifndef V5_ABL_NODMA
-#define V5_ABL_NODMA 0
-#endif
-#ifndef V5_ABL_NOKBAR
-#define V5_ABL_NOKBAR 0
-#endif
-#ifndef V5_ABL_NOEPI
-#define V5_ABL_NOEPI 0
-#endif
-constexpr int V5_BK = 32;
-constexpr int V5_TN = 128;                          // group tile: 256 rows x 128 columns
-constexpr int V5_AIMG = 256 * V5_BK;                // elements (16 KiB)
-constexpr int V5_SLOT = V5_AIMG + V5_TN * V5_BK;    // 24 KiB
-constexpr int V5_NSLOT = 3;
-constexpr int V5_CS = 2 * 128;                      // floats per group: column-sum partials [wr][128]
-
-// k-contiguous [rows][32] image: the 16-B chunk c of row r sits at chunk c ^ h(r), h(r) = -(r >> 2) mod 4.  The
-// 16x16x32 operand read (16 rows x 4 chunks, ds_read_b128 lane groups {0-3,12-15,20-27}, ...) then hits 16 distinct
-// 16-B bank groups in every lane group: conflict-free.
-VIT_DEV int v5_hk(int r) { return (-(r >> 2)) & 3; }
-
-template <bool KC>
-VIT_DEV bf16x8_t v5_frag(const bf16_t* img, int rb0, int lane) {
-  if (KC) {
-    const int r = rb0 + (lane & 15), c = lane >> 4;
-    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(img + r * V5_BK + ((c ^ v5_hk(r)) << 3)));
-  }
-  return read_frag<false>(img, rb0, 0, lane);        // [32 k][128] image, v4's row-strided layout and swizzle
-}
-
-// Byte offset (k = 0) of this lane's 16 B in LDS-DMA piece p.  KC: 16 rows x 64 B per piece (lane -> row lane / 4,
-// chunk lane % 4, the swizzle on the source); row-strided: 4 k-rows x 256 B.  Rows past the operand are clamped to
-// its last row / last 8 columns: their products land in outputs that are never stored.
-template <bool KC>
-VIT_DEV uint32_t v5_off(int64_t ld, int64_t rows, int64_t r0, int p, int lane) {
-  if (KC) {
-    const int row = p * 16 + (lane >> 2);
-    const int lc = (lane & 3) ^ v5_hk(row);
-    const int64_t gr = min(r0 + row, rows - 1);
-    return (uint32_t)((gr * ld + lc * 8) * 2);
-  }
-  const int kr = p * 4 + (lane >> 4);
-  const int c = (lane & 15) ^ swz_rs(kr);
-  const int64_t gr = min(r0 + c * 8, rows - 8);
-  return (uint32_t)((kr * ld + gr) * 2);
-}
-
-VIT_DEV void v5_dma(const char* src, const bf16_t* dst) {
-  const uint32_t lds =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)(dst));
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
-#pragma clang diagnostic pop
-}
-
-// vmcnt(n) for n = 0, 6, 12 (DMA pieces per wave per k-tile: 6)
-VIT_DEV void v5_wait(int n) {
-  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <bool BKC, int KIND, int ACT, bool MK, bool CS>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_v5(GemmArgs g, EpiParams e) {
-  // epilogue chunks: [LEAD: row-operand loads, bias -> LDS] 8 x [one 16-row block: 2 pieces] [CS: column-sum
-  // combine] [quiet] [quiet: vmcnt(0), barrier, next tile's first fragments]
-  constexpr int LEAD = KIND == EPI_PLAIN ? 0 : 2;
-  constexpr bool BIAS = KIND == EPI_BIAS_ACT || KIND == EPI_BDR;
-  constexpr int E = LEAD + 8 + (CS ? 1 : 0) + 2;
-  __shared__ __attribute__((aligned(16))) bf16_t smem5[2 * V5_NSLOT * V5_SLOT + 2 * V5_CS * 2 + 2 * V5_TN * 2];
-  const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, r16 = lane & 15;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2, gw = wave & 3, wr = gw >> 1, wc = gw & 1;
-  bf16_t* ring = smem5 + grp * V5_NSLOT * V5_SLOT;
-  float* csx = reinterpret_cast<float*>(smem5 + 2 * V5_NSLOT * V5_SLOT) + grp * V5_CS;
-  float* bsx = reinterpret_cast<float*>(smem5 + 2 * V5_NSLOT * V5_SLOT + 2 * V5_CS * 2) + grp * V5_TN;   // bias
-  // Items (group tiles) in XCD-contiguous ranges sized by the XCD's share of the workgroups (workgroups are dealt
-  // round-robin over the 8 XCDs: id % 8); the two groups of a workgroup take adjacent items (the same A row panel,
-  // L2-resident for both).
-  const int64_t nwg = gridDim.x, orig = blockIdx.x;
-  const int64_t xcd = orig % 8, wq = nwg / 8, wrm = nwg % 8;
-  const int64_t wb0 = xcd * wq + min(xcd, wrm), wb1 = (xcd + 1) * wq + min(xcd + 1, wrm);   // workgroups before / through
-  const int64_t lo = g.nitems * wb0 / nwg, hi = g.nitems * wb1 / nwg;
-  const int64_t sstep = 2 * (wb1 - wb0);
-  auto count = [&](int64_t first) { return first < hi ? (int)((hi - first + sstep - 1) / sstep) : 0; };
-  const int64_t first0 = lo + 2 * (orig / 8), first = first0 + grp;
-  const int n0 = count(first0), n1 = count(first0 + 1), nmine = grp ? n1 : n0;
-  const int nk = (int)(g.K / V5_BK);
-  const int P = nk + E;
-  constexpr int F = 3;                                  // fill: issue k-tiles 0-2 | - | wait, first fragments
-  const int off1 = (P + 1) / 2;                         // group 1 runs half a period behind group 0
-  const int n_iv = max(F + n0 * P, off1 + F + n1 * P);
-  const int off = grp ? off1 : 0;
-  // with >= 3 k-tiles the next tile's k-tiles 0-2 go out during this tile's last three k-steps (the ring simply
-  // continues: virtual k-tile nk + u); else behind the epilogue's stores
-  const bool early = nk >= 3;
-  const int nfill = min(3, nk);
-
-  const char* pa = (const char*)g.a;
-  const char* pb = (const char*)g.b;
-  const uint32_t sa = V5_BK * 2;                        // A is k-contiguous: bytes per k-tile
-  const uint32_t sb = BKC ? V5_BK * 2 : (uint32_t)(V5_BK * g.ldb * 2);
-  uint32_t oa[4], ob[2], oan[4], obn[2];                // DMA offsets of the k-loop's tile and of the next one
-  int64_t ki0 = 0, kj0 = 0, ktm = 0, ni0 = 0, nj0 = 0, ntm = 0;
-  int64_t ei0 = 0, ej0 = 0, etm = 0;                    // epilogue tile
-  auto set_next = [&](int idx) {                        // idx-th item of this group -> "next" coordinates + offsets
-    int64_t tm, tn, sidx;
-    v4_item(g, first + (int64_t)idx * sstep, tm, tn, sidx);
-    ntm = tm;
-    ni0 = tm * 256;
-    nj0 = tn * V5_TN;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) oan[i] = v5_off<true>(g.lda, g.M, ni0, gw * 4 + i, lane);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) obn[i] = v5_off<BKC>(g.ldb, g.N, nj0, gw * 2 + i, lane);
-  };
-  auto adopt_next = [&]() {
-    ktm = ntm;
-    ki0 = ni0;
-    kj0 = nj0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) oa[i] = oan[i];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) ob[i] = obn[i];
-  };
-  // piece k (0-3: A, 4-5: B) of k-tile u of the tile whose offsets are (xa, xb), into ring slot vs % 3
-  auto dma_piece = [&](const uint32_t (&xa)[4], const uint32_t (&xb)[2], int u, int vs, int k) {
-    bf16_t* slot = ring + (vs % V5_NSLOT) * V5_SLOT;
-    if (k < 4) v5_dma(pa + xa[k] + (uint32_t)u * sa, slot + (gw * 4 + k) * 512);
-    else v5_dma(pb + xb[k - 4] + (uint32_t)u * sb, slot + V5_AIMG + (gw * 2 + k - 4) * 512);
-  };
-
-  f32x4 acc[8][4];
-  bf16x8_t alo[4], ahi[4], bq[4];
-  uint4 pre[2][2];
-  float cs[2][8];
-  const int cq = (q & 1) * 16 + (q >> 1) * 8;           // the lane's 8 columns after swap16 (v4_epilogue_d)
-
-  auto barrier = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto first_frags = [&](int vs) {                      // zeroed accumulators, fragments x 0-3 and B of slot vs % 3
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-#pragma unroll
-      for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* slot = ring + (vs % V5_NSLOT) * V5_SLOT;
-#pragma unroll
-    for (int x = 0; x < 4; ++x) alo[x] = v5_frag<true>(slot, wr * 128 + x * 16, lane);
-#pragma unroll
-    for (int y = 0; y < 4; ++y) bq[y] = v5_frag<BKC>(slot + V5_AIMG, wc * 64 + y * 16, lane);
-  };
-  // row operands (residual / mask) of the pieces x (rows ei0 + wr*128 + 16x + r16, columns ej0 + wc*64 + 32yp + cq),
-  // in a 2-row-block ring two chunks ahead: x 0-1 in the first LEAD chunk, x + 2 behind piece x
-  auto load_pre = [&](int x) {
-    if (v4_has_pre<KIND>(e)) {
-#pragma unroll
-      for (int yp = 0; yp < 2; ++yp)
-        pre[x & 1][yp] = v4_pre_load8<KIND>(e, ei0 + wr * 128 + 16 * x + r16, ej0 + wc * 64 + 32 * yp + cq);
-    }
-  };
-  auto piece = [&](int x, int yp) {                     // rows 16x.. of the wave, 32-column half yp: math + stores
-    f32x4 y0 = acc[x][2 * yp], y1 = acc[x][2 * yp + 1];
-    swap16(y0, y1);
-    float v[8] = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
-    const int64_t i = ei0 + wr * 128 + 16 * x + r16, j = ej0 + wc * 64 + 32 * yp + cq;
-    uint32_t bits = 0u;
-    float b8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (BIAS) {                                         // the tile's bias columns, staged in LDS by the LEAD chunks
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(bsx + wc * 64 + 32 * yp + cq);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(bsx + wc * 64 + 32 * yp + cq + 4);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        b8[k] = b0[k];
-        b8[k + 4] = b1[k];
-      }
-    }
-    if (i < e.m && j < e.n) {
-      bits = v4_epi_row8<KIND, ACT, MK, CS>(e, i, j, (bf16_t*)e.c + i * e.ldc + j, b8, v,
-                                           v4_has_pre<KIND>(e) ? pre[x & 1][yp] : make_uint4(0u, 0u, 0u, 0u),
-                                           8 * (int)(i & 3));
-      if (CS) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) cs[yp][k] += v[k];
-      }
-    }
-    if (MK) {                                           // v4_epilogue_d: the quad of rows i..i+3 -> one 8-B store
-      int w = (int)(bits << (8 * (r16 & 3)));
-      w |= __builtin_amdgcn_mov_dpp(w, 0xB1, 0xF, 0xF, false);
-      w |= __builtin_amdgcn_mov_dpp(w, 0x4E, 0xF, 0xF, false);
-      if ((r16 & 3) == 0 && i < e.m && j < e.n) {
-        const uint32_t uw = (uint32_t)w;
-        *reinterpret_cast<uint2*>(e.mask_out + mask4_byte(i, j, e.n)) =
-            make_uint2(uw & 0x0f0f0f0fu, (uw >> 4) & 0x0f0f0f0fu);
-      }
-    }
-  };
-
-  // group 1's lead-in, then the fill
-#pragma unroll 1
-  for (int k = 0; k < off; ++k) __builtin_amdgcn_s_barrier();
-  if (nmine > 0) {
-    set_next(0);
-    adopt_next();
-    for (int u = 0; u < nfill; ++u)
-#pragma unroll
-      for (int k = 0; k < 6; ++k) dma_piece(oa, ob, u, u, k);
-  }
-  barrier();
-  barrier();
-  if (nmine > 0) v5_wait(6 * (nfill - 1));               // k-tile 0 landed (1, 2 may stay in flight)
-  barrier();
-  if (nmine > 0) first_frags(0);
-  int done = off + F;
-  int kbase = 0;                                        // virtual k-tile index of this tile's k-tile 0 (ring slot)
-
-#pragma unroll 1
-  for (int it = 0; it < nmine; ++it) {
-    const bool has_next = it + 1 < nmine;
-    if (has_next) set_next(it + 1);
-    const bool ahead = early && has_next;               // the next tile's k-tiles 0-2 go out in k-steps nk-3..nk-1
-    // ---- k-loop: one interval per 32-deep k-tile
-#pragma unroll 1
-    for (int t = 0; t < nk; ++t) {
-      const bf16_t* slot = ring + ((kbase + t) % V5_NSLOT) * V5_SLOT;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) ahi[x] = v5_frag<true>(slot, wr * 128 + (x + 4) * 16, lane);
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[y], alo[x], acc[x][y], 0, 0, 0);
-      if (t + 1 < nk) v5_wait(t + 2 < nk || ahead ? 6 : 0);     // k-tile t+1 landed (t+2 may stay in flight)
-      if (!V5_ABL_NOKBAR) barrier();
-      // k-tile t+3 (this tile's, or the next tile's t+3-nk) -> the slot of k-tile t (every wave's reads of it are
-      // done): its 6 pieces spread between the MFMAs (an LDS-DMA issue costs ~60 cycles of the wave's issue)
-      const int v = t + 3;
-      const bool dma = (v < nk || (ahead && v - nk < 3)) && !V5_ABL_NODMA;
-      const bool nxt = v >= nk;
-      const bool more = t + 1 < nk;
-      const bf16_t* nslot = ring + ((kbase + t + 1) % V5_NSLOT) * V5_SLOT;
-      if (more) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) alo[x] = v5_frag<true>(nslot, wr * 128 + x * 16, lane);
-      }
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          acc[x + 4][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[y], ahi[x], acc[x + 4][y], 0, 0, 0);
-          const int pc = y * 4 + x;                     // DMA pieces after MFMAs 1, 3, 5, 7, 9, 11
-          if (dma && (pc & 1) && pc < 12) {
-            if (nxt) dma_piece(oan, obn, v - nk, kbase + v, pc >> 1);
-            else dma_piece(oa, ob, v, kbase + v, pc >> 1);
-          }
-        }
-        if (more) bq[y] = v5_frag<BKC>(nslot + V5_AIMG, wc * 64 + y * 16, lane);
-      }
-    }
-    ei0 = ki0;
-    ej0 = kj0;
-    etm = ktm;
-    if (has_next) adopt_next();
-    kbase += nk;
-    // ---- epilogue: E chunks, one interval each
-#pragma unroll
-    for (int yp = 0; yp < 2; ++yp)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) cs[yp][k] = 0.f;
-    if (LEAD) {                                         // row operands of x 0-1; the bias columns -> LDS
-      load_pre(0);
-      load_pre(1);
-      float bias1 = 0.f;
-      const int64_t jb = ej0 + wc * 64 + lane;
-      if (BIAS && wr == 0 && e.bias && jb < e.n) bias1 = e.bias[jb];
-      barrier();
-      if (BIAS && wr == 0) bsx[wc * 64 + lane] = bias1;
-      barrier();
-    }
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {                       // one 16-row block per chunk: the stores spread evenly
-#pragma unroll
-      for (int yp = 0; yp < 2; ++yp)
-        if (!V5_ABL_NOEPI) piece(x, yp);
-      if (LEAD && x < 6) load_pre(x + 2);
-      if (CS && x == 7) {
-        // the wave's 128 rows: 16-lane butterfly (fixed order), lane r16 = 0 -> LDS partial [wr][column]
-#pragma unroll
-        for (int yp = 0; yp < 2; ++yp)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            float s_ = cs[yp][k];
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) s_ += __shfl_xor(s_, o, 16);
-            cs[yp][k] = s_;
-          }
-        if (r16 == 0) {
-#pragma unroll
-          for (int yp = 0; yp < 2; ++yp) {
-            float* d = csx + wr * 128 + wc * 64 + 32 * yp + cq;
-            *reinterpret_cast<f32x4*>(d) = f32x4{cs[yp][0], cs[yp][1], cs[yp][2], cs[yp][3]};
-            *reinterpret_cast<f32x4*>(d + 4) = f32x4{cs[yp][4], cs[yp][5], cs[yp][6], cs[yp][7]};
-          }
-        }
-      }
-      barrier();
-    }
-    if (CS) {                                           // row halves in fixed order -> one row of csum per tile
-      if (wr == 0) {
-        const int64_t j = ej0 + wc * 64 + lane;
-        if (j < e.n) e.csum[etm * e.n + j] = csx[wc * 64 + lane] + csx[128 + wc * 64 + lane];
-      }
-      barrier();
-    }
-    if (has_next && !early)                             // few k-tiles: the next tile's DMA behind every store
-      for (int u = 0; u < nfill; ++u)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dma_piece(oa, ob, u, kbase + u, k);
-    barrier();
-    if (has_next) {
-      if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // k-tiles 0-2 and the (older) stores
-      else v5_wait(6 * (nfill - 1));
-    }
-    barrier();
-    if (has_next) first_frags(kbase);
-    done += P;
-  }
-#pragma unroll 1
-  for (; done < n_iv; ++done) __builtin_amdgcn_s_barrier();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ------------------------------------------------------------------------------------------------------------
 // f32 MFMA kernel (exact fp32; generic strides; any M/N/K)
 // ------------------------------------------------------------------------------------------------------------
 constexpr int FBM = 64, FBK = 16, FPAD = 4;
@@ -1852,7 +1491,7 @@ bool aligned(const void* p, int a) { return p == nullptr || (((uintptr_t)p) % a)
 // span a 256 tile, else v2.
 int gemm_impl_env() {
   const int64_t v = vit::opt(vit::OPT_GEMM_IMPL);
-  return (v == 1 || v == 2 || v == 4 || v == 5) ? (int)v : 0;
+  return (v == 1 || v == 2 || v == 4) ? (int)v : 0;
 }
 
 int gemm_impl(int64_t m, int64_t n) {
@@ -1867,8 +1506,7 @@ int gemm_impl(int64_t m, int64_t n) {
 int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
   *m_main = d->m;
   if (d->split_k > 1 || d->in_dtype != VIT_BF16 || d->k % BK != 0 || d->m <= 0 || d->n <= 0) return 1;
-  const int impl = gemm_impl(d->m, d->n);
-  if ((impl != 4 && impl != 5) || d->out_group_rows != 0 || d->res_rowmod != 0) return 1;
+  if (gemm_impl(d->m, d->n) != 4 || d->out_group_rows != 0 || d->res_rowmod != 0) return 1;
   if (!vit::opt(vit::OPT_GEMM_TAIL)) return 1;
   const int64_t tn = (d->n + 255) / 256, tm = (d->m + 255) / 256, nkt = d->k / BK;
   const int64_t rounds = tm * tn / 256;
@@ -1899,7 +1537,7 @@ extern "C" int64_t vit_gemm_workspace_bytes(const vit_gemm_desc* d) {
 
 extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dtype) {
   if (m <= 0 || n <= 0 || k <= 0) return 1;
-  if (in_dtype == VIT_BF16 && k % BK == 0 && (gemm_impl(m, n) == 4 || gemm_impl(m, n) == 5)) {
+  if (in_dtype == VIT_BF16 && k % BK == 0 && gemm_impl(m, n) == 4) {
     const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
     // slices of >= 4 k-tiles; reductions of fewer than 16 k-tiles (the pruned last block's weight gradients: K = B)
     // may go down to 1 k-tile per slice (option splitk_min_kt overrides the minimum)
@@ -1993,7 +1631,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     const int impl = gemm_impl(d->m, d->n);
     const bool dma_ok = d->k % BK == 0 && a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL;
     const bool v2 = impl == 2 && dma_ok;
-    const bool v4 = (impl == 4 || impl == 3 || impl == 5) && dma_ok;
+    const bool v4 = (impl == 4 || impl == 3) && dma_ok;
     GemmArgs g4 = g;
     g4.tiles_n = (d->n + 255) / 256;
     g4.tiles_m = (d->m + 255) / 256;
@@ -2034,13 +1672,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     else if (out_bf && akc && !bkc && kind == EPI_AUXM) launched = EPI_AUXM;
     else if (out_bf && akc && bkc && kind == EPI_PATCH) launched = EPI_PATCH;
     if (launched != EPI_SLAB && launched != EPI_GENERAL && !e.vec8) launched = EPI_GENERAL;  // wide epilogue needs 8-wide rows
-    // v5 (two lock-stepped wave groups, epilogue beside the other group's k-loop): the k-contiguous-A layouts with a
-    // wide bf16 epilogue (no GELU, no patch remap), whole 32-deep k-tiles, no K split, persistent launches only
-    const bool v5 = impl == 5 && d->k % V5_BK == 0 && a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL && akc &&
-                    split == 1 && out_bf && e.act != VIT_ACT_GELU && !(d->flags & VIT_FLAG_SHARED_CUS) &&
-                    (launched == EPI_PLAIN || launched == EPI_BIAS_ACT || launched == EPI_BDR ||
-                     launched == EPI_AUX || launched == EPI_AUXM);
-    cs_fused = (v4 || v5) && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
+    cs_fused = v4 && d->colsum_part && launched != EPI_SLAB && launched != EPI_GENERAL;
     // persistent grid (one workgroup per CU looping over items) for the wide-epilogue kinds; option gemm_persist 0:
     // one workgroup per item (A/B switch)
     {
@@ -2049,40 +1681,6 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
       if (persist && g4.nitems > vit_cu_count()) grid4.x = (unsigned)vit_cu_count();
     }
     e.csum = cs_fused ? d->colsum_part : nullptr;
-    if (v5) {
-      GemmArgs g5 = g4;
-      g5.tiles_n = (d->n + V5_TN - 1) / V5_TN;
-      g5.tiles_m = (d->m + 255) / 256;
-      g5.group_m = g5.tiles_n >= 16 ? 8 : 1;
-      if (const int64_t gopt = vit::opt(vit::OPT_GEMM_GROUP_M)) g5.group_m = gopt;
-      g5.kt_per_split = d->k / V5_BK;
-      g5.nitems = g5.tiles_m * g5.tiles_n;
-      const unsigned grid5 = (unsigned)std::min<int64_t>(vit_cu_count(), (g5.nitems + 1) / 2);
-      const bool mk = e.mask_out != nullptr, cs = e.csum != nullptr;
-#define V5L(BKK, KIND, ACT, MK, CS) gemm_bf16_v5<BKK, KIND, ACT, MK, CS><<<grid5, 512, 0, s>>>(g5, e)
-#define V5MC(BKK, KIND, ACT)                      \
-  do {                                            \
-    if (mk && cs) V5L(BKK, KIND, ACT, true, true); \
-    else if (mk) V5L(BKK, KIND, ACT, true, false); \
-    else if (cs) V5L(BKK, KIND, ACT, false, true); \
-    else V5L(BKK, KIND, ACT, false, false);        \
-  } while (0)
-      if (bkc) {
-        if (launched == EPI_PLAIN) V5MC(true, EPI_PLAIN, 0);
-        else if (launched == EPI_BIAS_ACT && e.act == VIT_ACT_RELU) V5MC(true, EPI_BIAS_ACT, 1);
-        else if (launched == EPI_BIAS_ACT) V5MC(true, EPI_BIAS_ACT, 0);
-        else V5MC(true, EPI_BDR, 0);
-      } else {
-        if (launched == EPI_PLAIN) V5MC(false, EPI_PLAIN, 0);
-        else if (launched == EPI_AUX) V5MC(false, EPI_AUX, 0);
-        else V5MC(false, EPI_AUXM, 0);
-      }
-#undef V5MC
-#undef V5L
-      if (d->colsum_part && !cs_fused)
-        vit::colsum_parts_launch(d->c, d->ldc, d->out_dtype, d->m, d->n, 256, d->colsum_part, s);
-      return vit::check_launch("vit_gemm");
-    }
 #define V4(AK, BKK, TO, KIND) gemm_bf16_v4<AK, BKK, TO, KIND><<<grid4, 512, 0, s>>>(g4, e, a_bytes, b_bytes)
 #define LAUNCH_BF(AK, BKK)                                                                                     \
   do {                                                                                                         \
