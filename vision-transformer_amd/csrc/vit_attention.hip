@@ -766,6 +766,31 @@ VIT_DEV void rowsum32(const float (&t)[16], float (&u)[8]) {
 //   store(it-3): the staged dQ block -> global, full rows
 // P and dP of the block in flight stay in registers across the barrier.  No atomics, no cross-wave reduction of
 // results beyond the fixed-order delta sum: deterministic.
+// Diagnostic build only (-DATT_STAMPS=1, tools/attn_stamps.py): s_memtime stamps (lane 0 of every wave, workgroups
+// 0-15) of the fused backward's steady iterations (first item) and of whole items (first two), read back by
+// vit_diag_attn_stamps / vit_diag_attn_istamps.  Compiled out otherwise.
+#ifndef ATT_STAMPS
+#define ATT_STAMPS 0
+#endif
+#if ATT_STAMPS
+__device__ unsigned long long g_att_stamps[16 * 8 * 8 * 6];
+__device__ unsigned long long g_att_istamps[16 * 8 * 2 * 10];
+#define ATT_STAMP(IT, K)                                                                                   \
+  do {                                                                                                     \
+    if (item == (int64_t)blockIdx.x && blockIdx.x < 16 && lane == 0 && (IT) < 8)                           \
+      g_att_stamps[((blockIdx.x * 8 + wave) * 8 + (IT)) * 6 + (K)] = __builtin_amdgcn_s_memtime();          \
+  } while (0)
+#define ATT_ISTAMP(K)                                                                                      \
+  do {                                                                                                     \
+    const int64_t ii_ = (item - (int64_t)blockIdx.x) / gridDim.x;                                          \
+    if (blockIdx.x < 16 && lane == 0 && ii_ < 2)                                                           \
+      g_att_istamps[((blockIdx.x * 8 + wave) * 2 + ii_) * 10 + (K)] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
+#else
+#define ATT_STAMP(IT, K) do { } while (0)
+#define ATT_ISTAMP(K) do { } while (0)
+#endif
+
 template <int NQB>
 __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ d_o,
                                                          const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
@@ -870,9 +895,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     const int64_t nxt = item + gridDim.x;
     const bool more = nxt < items;
     const int64_t nb_ = more ? nxt / H : 0, nh_ = more ? nxt % H : 0;
+    ATT_ISTAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / V DMA, lse
     if (tid < Tp) lse2s[tid] = tid < Tn ? lreg * LOG2E : INFINITY;
     __syncthreads();                                  // every wave's DMA landed
+    ATT_ISTAMP(1);
     bf16x8_t kf[4], vf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -1018,19 +1045,37 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     if constexpr (NQB >= 3) {
       front(0);
       lds_barrier();
+      ATT_ISTAMP(2);
       back(0);
       front(1);
       if (wave >= 4) prefetch(-1);                    // dO block 0
       load_lse(more ? nxt : item);                    // after front(0) consumed the V fragments: no wait on it
       if (VLDS && !ATT_KVLDS) dma_slice_g(qkv, sb_ * Tn, ld, 2 * D + sh_ * HD, Tn, Tp, Vs, wave, lane);  // V: top only
       lds_barrier();
+      ATT_ISTAMP(3);
       back(1);
       front(2);
       dq(0);
       prefetch(0);                                    // Q block 0, dO block 1
       lds_barrier();
+      ATT_ISTAMP(4);
 #pragma unroll 1
       for (int it = 3; it < nqb; ++it) {
+        ATT_STAMP(it, 0);
+#if ATT_STAMPS
+        dq_store(it - 3);
+        ATT_STAMP(it, 1);
+        back(it - 1);
+        ATT_STAMP(it, 2);
+        front(it);
+        ATT_STAMP(it, 3);
+        dq(it - 2);
+        ATT_STAMP(it, 4);
+        prefetch(it - 2);
+        ATT_STAMP(it, 5);
+        lds_barrier();
+        continue;
+#endif
 #if ATT_ORDER == 1
         dq_store(it - 3);
         front(it);
@@ -1050,6 +1095,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         prefetch(it - 2);
         lds_barrier();                                // LDS only: the prefetch and the dQ stores stay in flight
       }
+      ATT_ISTAMP(5);
       dq_store(nqb - 3);
       back(nqb - 1);
       dq(nqb - 2);
@@ -1058,8 +1104,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       lds_barrier();
       dq_store(nqb - 2);
       dq(nqb - 1);
+      ATT_ISTAMP(6);
       if (wave < 4) prefetch(nqb - 1);                // Q block nqb-1
       lds_barrier();
+      ATT_ISTAMP(7);
       dq_store(nqb - 1);
     } else {                                          // T <= 64: the same schedule with its conditions
 #pragma unroll 1
@@ -1075,6 +1123,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       }
       dq_store(nqb - 1);
     }
+    ATT_ISTAMP(8);
     // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K
     dma_slice_g(qkv, sb_ * Tn, ld, D + sh_ * HD, Tn, Tp, Ks, wave, lane);
     if (kact && key < Tn) {
@@ -1092,6 +1141,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         }
       }
     }
+    ATT_ISTAMP(9);
   }
   // the last item re-staged its own K / Q / dO / V (dead blocks): retire that DMA before the LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1330,3 +1380,14 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
   }
   return vit::check_launch("vit_attn_bwd");
 }
+
+#if ATT_STAMPS
+extern "C" int vit_diag_attn_stamps(unsigned long long* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_stamps), std::min<int64_t>(n, 16 * 8 * 8 * 6) * 8) == hipSuccess
+             ? 0 : 1;
+}
+extern "C" int vit_diag_attn_istamps(unsigned long long* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_istamps), std::min<int64_t>(n, 16 * 8 * 2 * 10) * 8) == hipSuccess
+             ? 0 : 1;
+}
+#endif
