@@ -653,6 +653,14 @@ VIT_DEV bf16x8_t col_frag16(const bf16_t* img, int r0, int c0, int lane) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// An opaque copy of a per-lane index: values derived from it are recomputed where used instead of being hoisted out
+// of the persistent item loop.  The fused backward runs at the 256-VGPR limit, and a hoisted per-lane pointer is
+// spilled; the reload is a VMEM access whose s_waitcnt vmcnt(0) also drains the in-flight LDS-DMA prefetch.
+VIT_DEV int remat(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // LDS-DMA of one [Tp][64] head slice (rows of a row-major matrix with leading dim ld, columns col0..col0+63)
 // into a swizzled [Tp][64] image: 1 KiB pieces of 8 rows, lane-linear destination, the chunk swizzle applied to
 // the source address; rows >= Tn are zero-filled by an out-of-range offset.
@@ -699,6 +707,7 @@ VIT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 // backward masks them (P = 0 for queries >= T through lse = +inf, for keys >= T through kbias), finite data suffices.
 VIT_DEV void dma_piece(const bf16_t* base, int64_t row0, int64_t ld, int64_t col0, int Tn, bf16_t* img, int pc,
                        int lane) {
+  lane = remat(lane);
   const int r = pc * 8 + (lane >> 3);
   const int c = (lane & 7) ^ aswz(r);
   const bf16_t* src = base + (row0 + min(r, Tn - 1)) * ld + col0 + c * 8;
@@ -877,7 +886,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   // lse of item `it_` -> a register (tid < Tn <= 256)
   float lreg = 0.f;
   auto load_lse = [&](int64_t it_) {
-    if (tid < Tn) lreg = lse[it_ * Tn + tid];
+    const int t_ = remat(tid);
+    if (t_ < Tn) lreg = lse[it_ * Tn + t_];
   };
 
   int64_t item = blockIdx.x;
@@ -897,7 +907,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     const int64_t nb_ = more ? nxt / H : 0, nh_ = more ? nxt % H : 0;
     ATT_ISTAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / V DMA, lse
-    if (tid < Tp) lse2s[tid] = tid < Tn ? lreg * LOG2E : INFINITY;
+    {
+      const int t_ = remat(tid);
+      if (t_ < Tp) lse2s[t_] = t_ < Tn ? lreg * LOG2E : INFINITY;
+    }
     __syncthreads();                                  // every wave's DMA landed
     ATT_ISTAMP(1);
     bf16x8_t kf[4], vf[4];
@@ -958,8 +971,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 #endif
       // lane 16R (R = 16-lane row; hf = R >> 1) writes registers 8 (R & 1) + j: queries 16 (R & 1) + 4 hf + 0..3 and
       // 16 (R & 1) + 8 + 4 hf + 0..3
-      if ((lane & 15) == 0) {
-        float* dp = dpart + (qb & 1) * 256 + wave * 32 + 16 * ((lane >> 4) & 1) + 4 * hf;
+      const int ln_ = remat(lane);
+      if ((ln_ & 15) == 0) {
+        float* dp = dpart + (qb & 1) * 256 + wave * 32 + 16 * ((ln_ >> 4) & 1) + 4 * (ln_ >> 5);
         *reinterpret_cast<f32x4*>(dp) = f32x4{u[0], u[1], u[2], u[3]};
         *reinterpret_cast<f32x4*>(dp + 8) = f32x4{u[4], u[5], u[6], u[7]};
       }
