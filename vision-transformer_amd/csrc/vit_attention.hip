@@ -653,14 +653,6 @@ VIT_DEV bf16x8_t col_frag16(const bf16_t* img, int r0, int c0, int lane) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-// An opaque copy of a per-lane index: values derived from it are recomputed where used instead of being hoisted out
-// of the persistent item loop.  The fused backward runs at the 256-VGPR limit, and a hoisted per-lane pointer is
-// spilled; the reload is a VMEM access whose s_waitcnt vmcnt(0) also drains the in-flight LDS-DMA prefetch.
-VIT_DEV int remat(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
 // LDS-DMA of one [Tp][64] head slice (rows of a row-major matrix with leading dim ld, columns col0..col0+63)
 // into a swizzled [Tp][64] image: 1 KiB pieces of 8 rows, lane-linear destination, the chunk swizzle applied to
 // the source address; rows >= Tn are zero-filled by an out-of-range offset.

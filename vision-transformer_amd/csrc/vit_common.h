@@ -18,6 +18,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define VIT_DEV __device__ __forceinline__
 
+// An opaque copy of a per-lane index: values derived from it are recomputed where used instead of being hoisted out
+// of a persistent loop.  The persistent kernels run at the 256-VGPR limit, where a hoisted per-lane offset is spilled,
+// and a spill reload is a VMEM access whose s_waitcnt vmcnt(0) also drains the LDS-DMA loads in flight.
+VIT_DEV int remat(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 VIT_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 VIT_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, __float2bfloat16(f)); }
 

@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
   const uint32_t sa = AKC ? BK * 2 : (uint32_t)(BK * g.lda * 2);
   const uint32_t sb = BKC ? BK * 2 : (uint32_t)(BK * g.ldb * 2);
   uint32_t oa0[2], oa1[2], ob0[2], ob1[2];
-  v4_offsets<AKC, BKC>(g, i0, j0, sidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
+  v4_offsets<AKC, BKC>(g, i0, j0, sidx * g.kt_per_split * BK, wave, remat(lane), oa0, oa1, ob0, ob1);
   const char* pa_ = (const char*)g.a;
   const char* pb_ = (const char*)g.b;
 #define V4_DMA(R, P, OFF, SOFF, DST) dma_half_g(P, OFF, SOFF, DST, wave)
@@ -1345,15 +1345,14 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
       ni0 = ntm * 256;
       nj0 = ntn * 256;
       nnk = (int)max((int64_t)0, min(nkt, (nsidx + 1) * g.kt_per_split) - nsidx * g.kt_per_split);
-      v4_offsets<AKC, BKC>(g, ni0, nj0, nsidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
+      v4_offsets<AKC, BKC>(g, ni0, nj0, nsidx * g.kt_per_split * BK, wave, remat(lane), oa0, oa1, ob0, ob1);
       npre = min(V4_LEAD, 4 * nnk);
       for (int s = 0; s < npre; ++s) V4_STAGE(s);
     }
 
     // The epilogue's per-lane address arithmetic is loop-invariant; hoisted out of the persistent loop it stayed live
     // across the k-loop and spilled.  An opaque copy of tid makes the compiler recompute it per tile (a few dozen VALU).
-    int tid_e = tid;
-    asm volatile("" : "+v"(tid_e));
+    const int tid_e = remat(tid);
     if constexpr (WIDE) {
       float* csl = reinterpret_cast<float*>(smem4 + V4_SLOTS * HALF);
       if (KIND == EPI_BIAS_ACT && e.act == VIT_ACT_RELU) v4_epilogue_dd<KIND, 1>(e, acc, csl, tid_e, i0, j0, tm);
@@ -1375,7 +1374,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     nk = nnk;
     nstage = 4 * nk;
     // the offsets again (recomputed rather than kept live across the epilogue: register budget)
-    v4_offsets<AKC, BKC>(g, i0, j0, nsidx * g.kt_per_split * BK, wave, lane, oa0, oa1, ob0, ob1);
+    v4_offsets<AKC, BKC>(g, i0, j0, nsidx * g.kt_per_split * BK, wave, remat(lane), oa0, oa1, ob0, ob1);
     // stages 0..LEAD-1 went out before the epilogue; its loads and stores are younger, so retiring stages 0 and 1
     // waits for them too (vmcnt counts in order): wait for everything
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
