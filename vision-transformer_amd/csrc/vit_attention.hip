@@ -628,9 +628,6 @@ constexpr int FB_TMAX = 256;
 #ifndef ATT_PRIO                 // A/B builds only: s_setprio 1 around the S / dP MFMA chain
 #define ATT_PRIO 0
 #endif
-#ifndef ATT_ABL_NODELTA           // ablations for A/B builds only (tools/build_variant.sh): wrong results
-#define ATT_ABL_NODELTA 0
-#endif
 
 
 VIT_DEV __amdgpu_buffer_rsrc_t make_rsrc_b(const void* base, int64_t bytes) {
@@ -955,12 +952,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
       float t[16], u[8];
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = pc[r] * dpc[r];
-#if ATT_ABL_NODELTA
-#pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = t[j];
-#else
       rowsum32(t, u);
-#endif
       // lane 16R (R = 16-lane row; hf = R >> 1) writes registers 8 (R & 1) + j: queries 16 (R & 1) + 4 hf + 0..3 and
       // 16 (R & 1) + 8 + 4 hf + 0..3
       const int ln_ = remat(lane);
