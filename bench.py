@@ -261,7 +261,8 @@ def run(args, rank, world, local):
         torch.manual_seed(0)                       # identical init on every rank (reference init order, CPU RNG)
         model = vit.VisionTransformer(cfg).to(dev).train()
         if world > 1:
-            model.enable_data_parallel(grad_dtype=torch.bfloat16 if args.grad_comm == "bf16" else torch.float32)
+            model.enable_data_parallel(grad_dtype=torch.bfloat16 if args.grad_comm == "bf16" else torch.float32,
+                                       launch_mode=args.launch_mode)
         opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
         gen = torch.Generator().manual_seed(1234 + rank)
         x = torch.randn(args.batch, 3, args.img, args.img, generator=gen).to(dev)
@@ -350,6 +351,7 @@ def run(args, rank, world, local):
         if world > 1:
             out["comm_exposed_ms"] = round(comm, 3) if comm is not None else None
             out["grad_comm_dtype"] = args.grad_comm
+            out["launch_mode"] = args.launch_mode
         if args.dry_run:
             out["dry_run"] = True
             out["data"] = "dry run: CPU stand-in step on gloo, no HIP model (launch plumbing only)"
@@ -444,6 +446,9 @@ def main(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="dtype of the gradient all-reduce buckets for N > 1 (bf16: half the xGMI bytes)")
+    ap.add_argument("--launch-mode", default="auto", choices=["auto", "shared", "persistent"],
+                    help="N > 1: backward kernels beside RCCL as one workgroup per item (shared; auto on nccl) or "
+                         "persistent one-per-CU grids (DESIGN.md 5.4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events (profiling runs)")

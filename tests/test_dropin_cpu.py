@@ -339,6 +339,37 @@ def _ddp_worker(rank, world, port, q, comm_dtype=torch.float32):
     dist.destroy_process_group()
 
 
+def _launch_mode_worker(port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    m = vit.VisionTransformer(_cfg("micro"))
+    out = {}
+    for mode in ("auto", "shared", "persistent"):
+        out[mode] = m.enable_data_parallel(force=True, launch_mode=mode).hip_engine.shared_cus
+    try:
+        m.enable_data_parallel(force=True, launch_mode="bogus")
+        out["bad"] = "accepted"
+    except ValueError:
+        out["bad"] = "refused"
+    q.put(out)
+    dist.destroy_process_group()
+
+
+def test_enable_data_parallel_launch_mode():
+    """enable_data_parallel(launch_mode=...): 'auto' picks the shared-CU launch only on nccl (gloo here: persistent),
+    'shared' / 'persistent' force it (bench.py --launch-mode); anything else is refused."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_launch_mode_worker, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=120)
+    p.join(timeout=60)
+    assert out == {"auto": False, "shared": True, "persistent": False, "bad": "refused"}
+
+
 @pytest.mark.parametrize("comm_dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
 def test_ddp_gradient_buckets_gloo(comm_dtype):
     """2-rank gloo: every bucket of the flat gradient buffer is averaged across ranks; with bf16 buckets

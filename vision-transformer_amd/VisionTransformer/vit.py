@@ -95,23 +95,31 @@ class VisionTransformer(nn.Module):
             self._engine = Engine(self)
         return self._engine
 
-    def enable_data_parallel(self, group=None, force=False, grad_dtype=torch.float32):
+    def enable_data_parallel(self, group=None, force=False, grad_dtype=torch.float32, launch_mode="auto"):
         """Average gradients across the process group with RCCL, bucketed per block, overlapped with backward.
         `force` keeps the all-reduce path on even for a world of one rank (tests the collective on one GPU).
         `grad_dtype=torch.bfloat16` sends each bucket as bf16 (half the xGMI ring bytes): the fp32 gradients are
-        rounded to bf16, averaged in bf16 and widened back; master weights and optimizer state stay fp32."""
+        rounded to bf16, averaged in bf16 and widened back; master weights and optimizer state stay fp32.
+        `launch_mode` of the backward's GEMMs and fused attention backward beside the collectives: "shared" (one
+        workgroup per item, VIT_FLAG_SHARED_CUS), "persistent" (one workgroup per CU) or "auto" (shared on nccl,
+        where RCCL's kernels hold CUs).  Results are bitwise the same in every mode."""
         import torch.distributed as dist
         if not dist.is_initialized():
             raise RuntimeError("enable_data_parallel: torch.distributed is not initialised")
         if grad_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("enable_data_parallel: grad_dtype must be torch.float32 or torch.bfloat16")
+        if launch_mode not in ("auto", "shared", "persistent"):
+            raise ValueError("enable_data_parallel: launch_mode must be 'auto', 'shared' or 'persistent'")
         eng = self.hip_engine
         eng.ddp_group = group
         eng.comm_dtype = grad_dtype
         eng.ddp_enabled = bool(force) or dist.get_world_size(group) > 1
-        # RCCL's all-reduce kernels run on the GPU beside the backward: the backward's kernels then launch one
-        # workgroup per item instead of a persistent one-per-CU grid (VIT_FLAG_SHARED_CUS, vit_hip.h)
-        eng.shared_cus = eng.ddp_enabled and dist.get_backend(group) == "nccl"
+        # RCCL's all-reduce kernels run on the GPU beside the backward: by default the backward's kernels then launch
+        # one workgroup per item instead of a persistent one-per-CU grid (VIT_FLAG_SHARED_CUS, vit_hip.h)
+        if launch_mode == "auto":
+            eng.shared_cus = eng.ddp_enabled and dist.get_backend(group) == "nccl"
+        else:
+            eng.shared_cus = eng.ddp_enabled and launch_mode == "shared"
         return self
 
     # the engine holds a weakref to its model and views of the parameters: never copy or pickle it (a deep copy or
