@@ -748,6 +748,32 @@ VIT_DEV void rowsum32(const float (&t)[16], float (&u)[8]) {
 #undef VIT_DPP_ADD8
 }
 
+// A 32-row x 64-column block held as two 32x32 accumulators (rows on the lanes of each half-wave: lane (row, hf) holds
+// columns 8k + 4hf .. 8k + 4hf + 3 of group k = 4 db + g in registers 4g..4g+3 of acc[db]) stored as bf16 16-B row
+// pieces: one permlane32 swap per dword pairs groups (k, k + 1), as in the forward's O store.  `row` points at column
+// 8 hf of this lane's row; the swaps run on every lane, only the stores are predicated by `ok`.
+VIT_DEV void store_block_rows16(const f32x16 (&acc)[2], float mul, bf16_t* row, bool ok) {
+  uint32_t pk[8][2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = 4 * db + g;
+      pk[k][0] = (uint32_t)f2bf(acc[db][4 * g] * mul) | ((uint32_t)f2bf(acc[db][4 * g + 1] * mul) << 16);
+      pk[k][1] = (uint32_t)f2bf(acc[db][4 * g + 2] * mul) | ((uint32_t)f2bf(acc[db][4 * g + 3] * mul) << 16);
+    }
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(pk[k][w2], pk[k + 1][w2], false, false);
+      pk[k][w2] = sw[0];
+      pk[k + 1][w2] = sw[1];
+    }
+    if (ok) *reinterpret_cast<uint4*>(row + 8 * k) = make_uint4(pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]);
+  }
+}
+
 // Persistent: workgroup g handles items (image, head) g, g + gridDim.x, ...  The next item's operands are staged while
 // this one computes: its dO / Q 32-row blocks are LDS-DMA'd into this item's blocks as they die (dO block qb after
 // front(qb), Q block qb after back(qb)), its V after the first barrier, its K right after the last dQ block, its lse
@@ -1124,7 +1150,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
     ATT_ISTAMP(8);
     // K and dS^T are dead (the last dQ block ran before the final barrier): stage the next item's K
     dma_slice_g(qkv, sb_ * Tn, ld, D + sh_ * HD, Tn, Tp, Ks, wave, lane);
-    if (kact && key < Tn) {
+    if constexpr (NQB <= 7) {
+      if (kact) {                                     // dK / dV leave registers as 16-B row pieces
+        const int ln = remat(lane), key_ = kb + (ln & 31);
+        const int kr = key_ < Tn ? key_ : Tn - 1;      // (rows >= T: swaps only, no store)
+        bf16_t* dkr = dqkv + (b * Tn + kr) * ld + D + h * HD + 8 * (ln >> 5);
+        store_block_rows16(dk, scale, dkr, key_ < Tn);
+        store_block_rows16(dv, 1.f, dkr + D, key_ < Tn);
+      }
+    } else if (kact && key < Tn) {                    // NQB 8: 8-B pieces (the 16-B form spills there)
       bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD;
       bf16_t* dvr = dkr + D;
 #pragma unroll
