@@ -264,6 +264,33 @@ VIT_DEV f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 // row index (within a 32-row MFMA tile) of accumulator register r for lane half h
 VIT_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// A 32-row x 64-column block held as two 32x32 accumulators (rows on the lanes of each half-wave: lane (row, hf) holds
+// columns 8k + 4hf .. 8k + 4hf + 3 of group k = 4 db + g in registers 4g..4g+3 of acc[db]) stored as bf16 16-B row
+// pieces: one permlane32 swap per dword pairs groups (k, k + 1), as in the forward's O store.  `row` points at column
+// 8 hf of this lane's row; the swaps run on every lane, only the stores are predicated by `ok`.
+VIT_DEV void store_block_rows16(const f32x16 (&acc)[2], float mul, bf16_t* row, bool ok) {
+  uint32_t pk[8][2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int k = 4 * db + g;
+      pk[k][0] = (uint32_t)f2bf(acc[db][4 * g] * mul) | ((uint32_t)f2bf(acc[db][4 * g + 1] * mul) << 16);
+      pk[k][1] = (uint32_t)f2bf(acc[db][4 * g + 2] * mul) | ((uint32_t)f2bf(acc[db][4 * g + 3] * mul) << 16);
+    }
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(pk[k][w2], pk[k + 1][w2], false, false);
+      pk[k][w2] = sw[0];
+      pk[k + 1][w2] = sw[1];
+    }
+    if (ok) *reinterpret_cast<uint4*>(row + 8 * k) = make_uint4(pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]);
+  }
+}
+
+
 // XCD-aware (block, head) of a tiled kernel (1-D grid of nblk x B*H workgroups).  Workgroups are dealt round-robin
 // over the 8 XCDs (linear id % 8), each with its own L2; the nblk 128-row blocks of one (image, head) all stream the
 // head's whole K / V (or Q / dO), so in launch order they sat on nblk different XCDs and each fetched the head slice
@@ -357,20 +384,20 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_mfma(const bf16_t* __restrict
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = 1.0f / l_tot;
   const int64_t q = q0 + (lane & 31);
-  if (q < Tn) {
-    bf16_t* orow = o + (b * Tn + q) * D + h * HD;
+  const bool qok = q < Tn;
+  if (qok && o32) {
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float v[4] = {oacc[db][4 * g] * inv, oacc[db][4 * g + 1] * inv, oacc[db][4 * g + 2] * inv,
                       oacc[db][4 * g + 3] * inv};
-        st4<bf16_t>(orow + db * 32 + 8 * g + 4 * hf, v);
-        if (o32) st4<float>(o32 + (b * Tn + q) * D + h * HD + db * 32 + 8 * g + 4 * hf, v);
+        st4<float>(o32 + (b * Tn + q) * D + h * HD + db * 32 + 8 * g + 4 * hf, v);
       }
     }
-    if (hf == 0) lse[bh * Tn + q] = (m_run + log2f(l_tot)) / LOG2E;
   }
+  store_block_rows16(oacc, inv, o + (b * Tn + (qok ? q : Tn - 1)) * D + h * HD + 8 * hf, qok);
+  if (qok && hf == 0) lse[bh * Tn + q] = (m_run + log2f(l_tot)) / LOG2E;
 }
 
 // dQ of 128 queries per workgroup (4 waves x 32) over 64-key tiles.  It runs before attn_bwd_dkdv_mfma and forms
@@ -472,18 +499,7 @@ __global__ __launch_bounds__(256, ATT_DQ_MINB) void attn_bwd_dq_mfma(const bf16_
     tile_wait();
     __syncthreads();
   }
-  if (q < Tn) {
-    bf16_t* dst = dqkv + (b * Tn + q) * ld + h * HD;
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v[4] = {dq[db][4 * g] * scale, dq[db][4 * g + 1] * scale, dq[db][4 * g + 2] * scale,
-                      dq[db][4 * g + 3] * scale};
-        st4<bf16_t>(dst + db * 32 + 8 * g + 4 * hf, v);
-      }
-    }
-  }
+  store_block_rows16(dq, scale, dqkv + (b * Tn + (q < Tn ? q : Tn - 1)) * ld + h * HD + 8 * hf, q < Tn);
 }
 
 #ifndef ATT_DKDV_MINB            // A/B builds only: workgroups per CU the dK / dV kernel is sized for
@@ -589,21 +605,9 @@ __global__ __launch_bounds__(256, ATT_DKDV_MINB) void attn_bwd_dkdv_mfma(const b
     __syncthreads();
   }
   const int64_t key = k0 + (lane & 31);
-  if (key < Tn) {
-    bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD;
-    bf16_t* dvr = dkr + D;
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float a[4] = {dk[db][4 * g] * scale, dk[db][4 * g + 1] * scale, dk[db][4 * g + 2] * scale,
-                      dk[db][4 * g + 3] * scale};
-        float c[4] = {dv[db][4 * g], dv[db][4 * g + 1], dv[db][4 * g + 2], dv[db][4 * g + 3]};
-        st4<bf16_t>(dkr + db * 32 + 8 * g + 4 * hf, a);
-        st4<bf16_t>(dvr + db * 32 + 8 * g + 4 * hf, c);
-      }
-    }
-  }
+  bf16_t* dkr = dqkv + (b * Tn + (key < Tn ? key : Tn - 1)) * ld + D + h * HD + 8 * hf;
+  store_block_rows16(dk, scale, dkr, key < Tn);
+  store_block_rows16(dv, 1.f, dkr + D, key < Tn);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -746,32 +750,6 @@ VIT_DEV void rowsum32(const float (&t)[16], float (&u)[8]) {
   VIT_DPP_ADD8("quad_perm:[2,3,0,1]");
   VIT_DPP_ADD8("quad_perm:[1,0,3,2]");
 #undef VIT_DPP_ADD8
-}
-
-// A 32-row x 64-column block held as two 32x32 accumulators (rows on the lanes of each half-wave: lane (row, hf) holds
-// columns 8k + 4hf .. 8k + 4hf + 3 of group k = 4 db + g in registers 4g..4g+3 of acc[db]) stored as bf16 16-B row
-// pieces: one permlane32 swap per dword pairs groups (k, k + 1), as in the forward's O store.  `row` points at column
-// 8 hf of this lane's row; the swaps run on every lane, only the stores are predicated by `ok`.
-VIT_DEV void store_block_rows16(const f32x16 (&acc)[2], float mul, bf16_t* row, bool ok) {
-  uint32_t pk[8][2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int k = 4 * db + g;
-      pk[k][0] = (uint32_t)f2bf(acc[db][4 * g] * mul) | ((uint32_t)f2bf(acc[db][4 * g + 1] * mul) << 16);
-      pk[k][1] = (uint32_t)f2bf(acc[db][4 * g + 2] * mul) | ((uint32_t)f2bf(acc[db][4 * g + 3] * mul) << 16);
-    }
-#pragma unroll
-  for (int k = 0; k < 8; k += 2) {
-#pragma unroll
-    for (int w2 = 0; w2 < 2; ++w2) {
-      const auto sw = __builtin_amdgcn_permlane32_swap(pk[k][w2], pk[k + 1][w2], false, false);
-      pk[k][w2] = sw[0];
-      pk[k + 1][w2] = sw[1];
-    }
-    if (ok) *reinterpret_cast<uint4*>(row + 8 * k) = make_uint4(pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]);
-  }
 }
 
 // Persistent: workgroup g handles items (image, head) g, g + gridDim.x, ...  The next item's operands are staged while
