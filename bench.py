@@ -377,6 +377,10 @@ def run(args, rank, world, local):
                 out["roofline"] = {
                     "bound": bound, "family": dom, "achieved": ach, "peak": pk, "unit": unit,
                     "frac": round(ach / pk, 4),
+                    "frac_basis": "FLOPs the family's launches execute (the pruned last block charged for its B "
+                                  "token-0 rows only)" if bound == "mfma" else "algorithmic bytes",
+                    # whole step, executed FLOPs (step_mfma_frac credits the reference's FLOPs, pruned rows included)
+                    "step_frac_executed": out["step_mfma_frac_executed"],
                     # per launch, like `achieved`: the PMC family's HBM bytes per step / this family's launches
                     "traffic": int(traffic / d["launches_per_step"]) if traffic is not None else None,
                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE)",
@@ -447,8 +451,8 @@ def main(argv=None):
     ap.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                     help="dtype of the gradient all-reduce buckets for N > 1 (bf16: half the xGMI bytes)")
     ap.add_argument("--launch-mode", default="auto", choices=["auto", "shared", "persistent"],
-                    help="N > 1: backward kernels beside RCCL as one workgroup per item (shared; auto on nccl) or "
-                         "persistent one-per-CU grids (DESIGN.md 5.4)")
+                    help="N > 1: backward kernels beside RCCL as persistent one-per-CU grids (persistent; auto) or "
+                         "one workgroup per item (shared) (DESIGN.md 5.4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-peak", action="store_true", help="skip the measured 8192^3 GEMM peak (profiling runs)")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events (profiling runs)")

@@ -481,10 +481,14 @@ def test_missing_library_fails_loudly(monkeypatch):
         m(x.to(DEV))
 
 
-def _engine_vs_oracle_on_gpu(ocfg, seed):
-    """bf16 TRAIN-mode engine run vs the oracle evaluated on the GPU with torch ops, gated by the spread of valid bf16
-    evaluations (fp32 / fp64 / flash rounding between the same storage points): logits 1e-2; each gradient (q/k per
-    block, all heads together) <= max(1e-2, 2 x spread); the whole vector likewise."""
+def _engine_vs_oracle_on_gpu(ocfg, seed, full_depth=False):
+    """bf16 TRAIN-mode engine run vs the oracle evaluated on the GPU with torch ops.  Depth 2 (full_depth False):
+    logits within 1e-2 of the bf16 oracle; each gradient (q/k per block, all heads together) <= max(1e-2, 2 x the
+    spread of valid bf16 evaluations: fp32 / fp64 / flash rounding between the same storage points); the whole vector
+    likewise.  full_depth: at depth 12 the valid bf16 evaluations themselves disagree by ~46% in the logits (the
+    saturating x sqrt(hd) softmax turns rounding differences into different attention argmaxes), so no elementwise
+    gate is meaningful there; the run is a property check — finite, and the mean loss within 2e-2 (relative) of the
+    fp32 oracle's — and per-block parity at that depth is test_vit_base_depth12_teacher_forced_blocks_bf16."""
     st = O.init_state(ocfg, seed=seed)
     m = _model(ocfg, st, torch.bfloat16).train()
     x, y = O.synthetic_batch(ocfg)
@@ -493,24 +497,28 @@ def _engine_vs_oracle_on_gpu(ocfg, seed):
     base_seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
     torch.manual_seed(5)
     logits = m(xd)
-    cross_entropy(logits, yd).backward()
+    loss = cross_entropy(logits, yd)
+    loss.backward()
     ours = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
-    logits = logits.detach()
+    logits, loss = logits.detach(), float(loss)
     del m
     torch.cuda.empty_cache()
     sd = {k: v.to(DEV) for k, v in st.items()}
     kw = dict(train=True, seed=base_seed)
-    lg_bf, _, g_bf = O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, **kw)
-    lg_32, _, g_32 = O.loss_and_grads(sd, xd, yd, ocfg, **kw)
+    lg_bf, loss_bf, g_bf = O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, **kw)
+    lg_32, loss_32, g_32 = O.loss_and_grads(sd, xd, yd, ocfg, **kw)
     lg_64, _, g_64 = O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, dtype=torch.float64, **kw)
     lg_fl, _, g_fl = O.loss_and_grads(sd, xd, yd, ocfg, bf16=True, flash=True, **kw)
     valid = [g_bf, g_64, g_fl]
-    # logits: within 1e-2 of the bf16 oracle, or (deep stacks, where the x sqrt(hd) softmax turns bf16 rounding
-    # differences into different attention argmaxes) within 2x the spread of the valid bf16 evaluations around fp32
     lspread = max(_rel(v, lg_32) for v in (lg_bf, lg_64, lg_fl))
     print(f"logits: vs bf16 oracle {_rel(logits, lg_bf):.3e}, vs fp32 {_rel(logits, lg_32):.3e}, "
-          f"valid-bf16 spread {lspread:.3e}")
-    assert _rel(logits, lg_bf) < 1e-2 or _rel(logits, lg_32) <= 2 * lspread, (_rel(logits, lg_bf), lspread)
+          f"valid-bf16 spread {lspread:.3e}; loss ours {loss:.5f} bf16 oracle {float(loss_bf):.5f} "
+          f"fp32 {float(loss_32):.5f}")
+    if full_depth:
+        assert np.isfinite(loss) and all(bool(torch.isfinite(g).all()) for g in ours.values())
+        assert abs(loss - float(loss_32)) <= 2e-2 * abs(float(loss_32)), (loss, float(loss_32))
+        return
+    assert _rel(logits, lg_bf) < 1e-2, _rel(logits, lg_bf)
 
     def err(g, keys):
         a = torch.cat([g[k].reshape(-1).double() for k in keys])
@@ -540,11 +548,99 @@ def test_c2_full_shape_bf16_train_vs_oracle():
     two blocks (block 0 runs every GEMM at full M with dense gradients; block 1 is the pruned last block), through the
     engine, against the oracle evaluated on the GPU with torch ops.  This brings the full-size kernels under parity
     test: the K = 50,432 split-K weight-gradient GEMMs, the persistent many-round forward / dgrad GEMMs (591-2,364
-    tiles) and their split-K tails, the 3,072-item persistent attention backward.  Gates of _engine_vs_oracle_on_gpu."""
+    tiles) and their split-K tails, the 3,072-item persistent attention backward.  Gates of _engine_vs_oracle_on_gpu
+    (logits 1e-2 vs the bf16 oracle, hard)."""
     _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=256, blocks=2, num_classes=1000), seed=23)
 
 
-def test_vit_base_full_depth_bf16_train_vs_oracle():
-    """ViT-B/16 at FULL depth (12 blocks, transformer.py:82-90), 224^2, B=8, bf16, train mode, through the engine vs the
-    oracle on the GPU (VERDICT r3 #4): the 12-block bf16 path under the same spread gates as the 2-block tests."""
-    _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=8, blocks=12, num_classes=1000), seed=29)
+def test_vit_base_full_depth_bf16_train_properties():
+    """ViT-B/16 at FULL depth (12 blocks, transformer.py:82-90), 224^2, B=8, bf16, train mode, through the engine:
+    a property check only (finite; loss within 2e-2 of the fp32 oracle's).  Elementwise parity at depth 12 is gated
+    per block by the teacher-forced test below and end to end in fp32 by test_vit_base_full_depth_fp32_vs_fp64."""
+    _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=8, blocks=12, num_classes=1000), seed=29,
+                             full_depth=True)
+
+
+def test_vit_base_depth12_teacher_forced_blocks_bf16():
+    """Per-block bf16 parity at C2 widths through depth 12, teacher-forced: the oracle runs the whole
+    ViT-B/16 (224^2, B=8, train mode, counter-hash dropout) in fp32 and records every block's input and the loss
+    gradient at every block's output; each engine block (Engine.block_forward / block_backward: the fused kernels of
+    the whole-model path) is then fed THAT block's input and output gradient, rounded to bf16, so errors cannot
+    compound across depth.  Per block, against the oracle block that rounds to bf16 at the same storage points:
+      * block output and input gradient within 1e-2 (norm-wise) of the bf16 oracle;
+      * every weight gradient (per-head q / k / v of a block concatenated) within max(1e-2, 2x the spread of the
+        valid bf16 evaluations — fp32 / fp64 arithmetic, flash rounding — around the fp64 one) of the fp64 one."""
+    ocfg = O.make_config("base", img=224, batch=8, num_classes=1000)
+    L, B, T, D, H = ocfg.num_blocks, ocfg.batch_size, ocfg.T, ocfg.embedding_size, ocfg.num_heads
+    M = B * T
+    st = O.init_state(ocfg, seed=29)
+    m = _model(ocfg, st, torch.bfloat16).train()
+    x, y = O.synthetic_batch(ocfg)
+    xd, yd = x.to(DEV), y.to(DEV)
+    seed = 987654321
+    sd = {k: v.to(DEV) for k, v in st.items()}
+    # the teacher: fp32 oracle forward / backward, every block's output kept with its gradient
+    e = O.embed_forward(sd, xd, ocfg).detach().requires_grad_(True)
+    ins, outs = [], []
+    for l in range(L):
+        ins.append(e)
+        e, _ = O.block_forward(sd, l, e, ocfg, train=True, seed=seed)
+        e.retain_grad()
+        outs.append(e)
+    torch.nn.functional.cross_entropy(O.head_forward(sd, e), yd).backward()
+    eng = m.hip_engine
+    eng.ensure_ready(xd.device)
+    req = {k: True for k in eng.owners}
+    rnd = O._RoundBF16.apply
+    names = ["qkv_w", "proj_w", "proj_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b", "ln1_w", "ln1_b", "ln2_w", "ln2_b"]
+    bad, report = [], []
+    for l in range(L):
+        x_in = ins[l].detach().bfloat16()
+        dy = outs[l].grad.detach().bfloat16()
+        # ---- engine block
+        x_out, saved = eng.block_forward(l, x_in.view(M, D).contiguous(), B, True, seed, True)
+        eng.G.zero_()
+        dxo = dy.view(M, D).contiguous()
+        g1 = _ops.mask4_apply(dxo, torch.empty_like(dxo), saved[15], 1.0)
+        dx_in, _ = eng.block_backward(l, saved, dxo, g1, False, 0.0, req, None, True, B)
+        torch.cuda.synchronize()
+        ours = {n: eng.gw[f"{l}.{n}"].double().clone() for n in names}
+
+        # ---- oracle block between the same bf16 storage points: fp32 / fp64 arithmetic, flash rounding
+        def oracle_block(dtype, flash=False):
+            pre = f"transformer_encoder.blocks.{l}."
+            p = {k: v.to(dtype).clone().requires_grad_(True) for k, v in sd.items() if k.startswith(pre)}
+            xi = x_in.to(dtype).requires_grad_(True)
+            yo, _ = O.block_forward(p, l, xi, ocfg, rnd, train=True, seed=seed, flash=flash)
+            yo.backward(dy.to(dtype))
+            q = [p[pre + f"multi_head.heads.{h}.query.weight"].grad for h in range(H)]
+            k = [p[pre + f"multi_head.heads.{h}.key.weight"].grad for h in range(H)]
+            v = [p[pre + f"multi_head.heads.{h}.value.weight"].grad for h in range(H)]
+            g = {"qkv_w": torch.cat(q + k + v, 0), "proj_w": p[pre + "multi_head.proj.weight"].grad,
+                 "proj_b": p[pre + "multi_head.proj.bias"].grad, "fc1_w": p[pre + "ffwd.mlp.0.weight"].grad,
+                 "fc1_b": p[pre + "ffwd.mlp.0.bias"].grad, "fc2_w": p[pre + "ffwd.mlp.2.weight"].grad,
+                 "fc2_b": p[pre + "ffwd.mlp.2.bias"].grad, "ln1_w": p[pre + "ln1.weight"].grad,
+                 "ln1_b": p[pre + "ln1.bias"].grad, "ln2_w": p[pre + "ln2.weight"].grad,
+                 "ln2_b": p[pre + "ln2.bias"].grad}
+            return yo.detach(), xi.grad.detach(), {n: t.double() for n, t in g.items()}
+
+        y_bf, dx_bf, g_bf = oracle_block(torch.float32)
+        _, _, g_64 = oracle_block(torch.float64)
+        _, _, g_fl = oracle_block(torch.float32, flash=True)
+        e_out = _rel(x_out.view(B, T, D), y_bf)
+        e_dx = _rel(dx_in.view(B, T, D), dx_bf)
+        report.append((l, "out", e_out))
+        report.append((l, "dx", e_dx))
+        if e_out >= 1e-2 or e_dx >= 1e-2:
+            bad.append((l, "out/dx", e_out, e_dx))
+        for n in names:
+            e_ours = _rel(ours[n], g_64[n])
+            spread = max(_rel(g_bf[n], g_64[n]), _rel(g_fl[n], g_64[n]))
+            report.append((l, n, e_ours, spread))
+            if e_ours > max(1e-2, 2 * spread):
+                bad.append((l, n, e_ours, spread))
+        del saved, x_out, dx_in
+    print("teacher-forced per-block errors:")
+    for r in report:
+        print("  ", r)
+    assert not bad, bad

@@ -394,3 +394,54 @@ def test_full_size_configs_properties(preset, img, batch):
         opt.step()
         losses.append(loss.item())
     assert losses[2] < losses[0], losses
+
+
+def test_vit_base_full_depth_fp32_vs_fp64():
+    """ViT-B/16 at FULL depth (12 blocks, transformer.py:82-90), 224^2, B=8, fp32, eval mode, through the engine vs the
+    oracle evaluated on the GPU in fp64.  Gates: logits max-abs error vs fp64 <=
+    max(1e-4, 2x the fp32 oracle's (torch GEMMs: what the reference runs) error vs fp64); every gradient per tensor
+    within max(2e-4, 8x the larger error of two valid fp32 summation orders — the torch one and the oracle with
+    sequential-chain accumulation, this path's order) vs fp64, and the whole gradient vector within 2x the
+    sequential-order sample (the rule of test_tiny_c1_fp32_vs_reference)."""
+    ocfg = O.make_config("base", img=224, batch=8, num_classes=1000)
+    st = O.init_state(ocfg, seed=31)
+    m = _model(ocfg)
+    m.load_state_dict(st)
+    m.eval()
+    x, y = O.synthetic_batch(ocfg)
+    xd, yd = x.to(DEV), y.to(DEV)
+    logits = m(xd)
+    cross_entropy(logits, yd).backward()
+    ours = {k: p.grad.detach().double() for k, p in m.named_parameters()}
+    logits = logits.detach().double()
+    del m
+    torch.cuda.empty_cache()
+    sd = {k: v.to(DEV) for k, v in st.items()}
+    lg32, _, g32 = O.loss_and_grads(sd, xd, yd, ocfg)
+    lg64, _, g64 = O.loss_and_grads(sd, xd, yd, ocfg, dtype=torch.float64)
+    lgsq, _, gsq = O.loss_and_grads(sd, xd, yd, ocfg, seq_chain=True)
+    ref_err = float((lg32.double() - lg64).abs().max())
+    seq_err = float((lgsq.double() - lg64).abs().max())
+    our_err = float((logits - lg64).abs().max())
+    print(f"logits max-abs vs fp64: ours {our_err:.3e}, oracle fp32 {ref_err:.3e}, seq-chain {seq_err:.3e}")
+    assert our_err <= max(1e-4, 2 * ref_err), (our_err, ref_err)
+    worst, bad = [], []
+    cat = {"ours": [], "seq": [], "r64": []}
+    for k in g64:
+        r64 = g64[k].reshape(-1)
+        n64 = max(float(r64.norm()), 1e-30)
+        e_ours = float((ours[k].reshape(-1) - r64).norm()) / n64
+        e_ref = max(float((g32[k].double().reshape(-1) - r64).norm()),
+                    float((gsq[k].double().reshape(-1) - r64).norm())) / n64
+        worst.append((e_ours / max(e_ref, 1e-12), k, e_ours, e_ref))
+        if e_ours > max(2e-4, 8 * e_ref):
+            bad.append((k, e_ours, e_ref))
+        cat["ours"].append(ours[k].reshape(-1))
+        cat["seq"].append(gsq[k].double().reshape(-1))
+        cat["r64"].append(r64)
+    print("worst gradient error ratios (ours / valid-order error):", sorted(worst)[-4:])
+    assert not bad, bad
+    o, sq, r = (torch.cat(cat[n_]) for n_ in ("ours", "seq", "r64"))
+    e_all, e_sq = float((o - r).norm()), float((sq - r).norm())
+    print(f"whole gradient vector: ours {e_all / float(r.norm()):.3e}, seq-chain {e_sq / float(r.norm()):.3e}")
+    assert e_all <= max(1e-5 * float(r.norm()), 2 * e_sq)

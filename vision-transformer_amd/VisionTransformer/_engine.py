@@ -228,6 +228,7 @@ class Engine:
 
         # per-parameter grad view + shadow view (the optimizer refreshes the shadow in its kernel)
         self.grad_views = []
+        self.grad_region = []           # gradient region (key of self.gw / self.owners) of each grad view
         self.pack_entries = []
         for name, p in params.items():
             l, _, short = name.partition(".") if "." in name else ("", "", name)
@@ -236,10 +237,12 @@ class Engine:
                 row0 = {"q": 0, "k": D, "v": 2 * D}[short[0]] + h * hd
                 gv = self.gw[f"{l}.qkv_w"][row0:row0 + hd]
                 sv = self.ww[f"{l}.qkv_w"][row0:row0 + hd]
+                self.grad_region.append(f"{l}.qkv_w")
             else:
                 key = name
                 gv = self.gw[key].view(p.shape)
                 sv = self.ww[key].view(p.shape) if key in self.ww else None
+                self.grad_region.append(key)
             self.grad_views.append((p, gv))
             SHADOWS[p] = sv
             if sv is not None:
@@ -392,7 +395,6 @@ class Engine:
     # forward
     # ------------------------------------------------------------------------------------------------------------
     def forward(self, x, training, save, want_probs=False):
-        model = self.model_ref()
         if not x.is_cuda:
             raise RuntimeError("VisionTransformer (HIP path) needs the input on a ROCm device; there is no CPU path")
         if x.dim() != 4 or x.shape[1] != self.C or x.shape[2] % self.P or x.shape[3] % self.P:
@@ -410,7 +412,7 @@ class Engine:
         x = x.contiguous()
         if x.dtype not in (torch.float32, torch.bfloat16):
             x = x.float()
-        D, T, N, H, hd, L, dt = self.D, self.T, self.N, self.H, self.hd, self.L, self.dtype
+        D, T, N, L, dt = self.D, self.T, self.N, self.L, self.dtype
         M = B * T
         es = 2 if dt == torch.bfloat16 else 4
         prm = self.params
@@ -431,62 +433,10 @@ class Engine:
         # (rows b*T, row stride T*D; dropout bits drawn at the full tensor's indices) — the same logits, loss and
         # gradients as computing all B*T rows and discarding the rest.  `prune_last = False` computes every row.
         prune = self.prune_last
-        drop_p = DROPOUT_P if training else 0.0
-        keep_masks = save and training          # the backward reads the forward's dropout keep bits (mask4)
         for l in range(L):
-            blk = model.transformer_encoder.blocks[l]
-            x_in = xcur
-            ln_b = 2 * M * D * es + 8 * M
-            mk("ln_fwd", 0, 0.0, ln_b)
-            a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
-            mk("ln_fwd", 1)
-            mk("gemm_fwd", 0, 2.0 * M * 3 * D * D, (M * D + 3 * D * D + 3 * M * D) * es)
-            qkv = _ops.linear(a1, self.ww[f"{l}.qkv_w"])                                # 3H heads' K/Q/V in one GEMM
-            mk("gemm_fwd", 1)
-            probs = None
-            if want_probs:
-                probs = torch.empty(B, H, T, T, dtype=torch.float32, device=x.device)
-            # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta; the
-            # fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
-            o32 = (torch.empty(M, D, dtype=torch.float32, device=x.device)
-                   if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
-            mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
-                                                                                         else 0))
-            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
-            mk("attn_fwd", 1)
-            blk.multi_head.attention_probs = probs
-            blk.multi_head._probs_skipped = probs is None       # a later read warns once (transformer.py)
-            # rows of the post-attention part: all M, or (last block, pruned) the B token-0 rows b*T
-            pr = prune and l == L - 1
-            R, rs = (B, T) if pr else (M, 1)
-            pm = _ops.mask4_empty(R, D, x.device) if keep_masks else None      # proj dropout keep bits
-            fm = _ops.mask4_empty(R, D, x.device) if keep_masks else None      # fc2 dropout keep bits
-            x_mid = torch.empty(R, D, dtype=dt, device=x.device)
-            mk("gemm_fwd", 0, 2.0 * R * D * D, (3 * R * D + D * D) * es)
-            self._gemm_rows(pr, o, self.ww[f"{l}.proj_w"], x_mid, R, D, D, rs * D, D, D, bias=prm[f"{l}.proj_b"],
-                            res=x_in, ldres=rs * D, dropout_p=drop_p, seed=site_seed(seed, l, 0),
-                            drop_row_stride=rs, mask_out=pm)
-            mk("gemm_fwd", 1)
-            mk("ln_fwd", 0, 0.0, 2 * R * D * es + 8 * R)
-            a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
-            mk("ln_fwd", 1)
-            # saved for the backward: the ReLU mask as 1 bit per element (mask4, read by fc2's dgrad epilogue instead
-            # of re-reading h: 1/16 of the bytes)
-            hm = _ops.mask4_empty(R, 4 * D, x.device) if save else None
-            mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + (R * D // 2 if save else 0))
-            h = torch.empty(R, 4 * D, dtype=dt, device=x.device)
-            self._gemm_rows(pr, a2, self.ww[f"{l}.fc1_w"], h, R, 4 * D, D, D, D, 4 * D, bias=prm[f"{l}.fc1_b"],
-                            act=ACT_RELU, mask_out=hm)
-            mk("gemm_fwd", 1)
-            x_out = torch.empty(R, D, dtype=dt, device=x.device)
-            mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + 2 * R * D) * es)
-            self._gemm_rows(pr, h, self.ww[f"{l}.fc2_w"], x_out, R, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
-                            res=x_mid, ldres=D, dropout_p=drop_p, seed=site_seed(seed, l, 1), drop_row_stride=rs,
-                            mask_out=fm)
-            mk("gemm_fwd", 1)
+            xcur, saved = self.block_forward(l, xcur, B, training, seed, save, want_probs, prune and l == L - 1)
             if save:
-                blocks.append((x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm))
-            xcur = x_out
+                blocks.append(saved)
         # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
         z = torch.empty(B, D, dtype=torch.float32, device=x.device)
         _ops.copy2d(xcur, D if prune else T * D, z, D, B, D)
@@ -500,6 +450,70 @@ class Engine:
             tape.z, tape.u, tape.gz, tape.zn, tape.mh, tape.rh = z, u, gz, zn, mh, rh
             tape.seed, tape.training, tape.pruned = seed, training, prune
         return logits, tape
+
+    def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False):
+        """Block l (transformer.py:76-79) on x_in [B*T, D] (compute dtype): x_mid = x_in + drop(MHA(ln1(x_in))),
+        x_out = x_mid + drop(FFN(ln2(x_mid))).  `pr`: the post-attention part on the B token-0 rows only (the pruned
+        last block).  Returns (x_out, saved): `saved` is what block_backward needs (None unless `save`)."""
+        model = self.model_ref()
+        D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
+        M = B * T
+        es = 2 if dt == torch.bfloat16 else 4
+        prm = self.params
+        mk = self._mark
+        drop_p = DROPOUT_P if training else 0.0
+        keep_masks = save and training          # the backward reads the forward's dropout keep bits (mask4)
+        dev = x_in.device
+        blk = model.transformer_encoder.blocks[l]
+        ln_b = 2 * M * D * es + 8 * M
+        mk("ln_fwd", 0, 0.0, ln_b)
+        a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
+        mk("ln_fwd", 1)
+        mk("gemm_fwd", 0, 2.0 * M * 3 * D * D, (M * D + 3 * D * D + 3 * M * D) * es)
+        qkv = _ops.linear(a1, self.ww[f"{l}.qkv_w"])                                # 3H heads' K/Q/V in one GEMM
+        mk("gemm_fwd", 1)
+        probs = None
+        if want_probs:
+            probs = torch.empty(B, H, T, T, dtype=torch.float32, device=dev)
+        # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta; the
+        # fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
+        o32 = (torch.empty(M, D, dtype=torch.float32, device=dev)
+               if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
+        mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
+                                                                                     else 0))
+        o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
+        mk("attn_fwd", 1)
+        blk.multi_head.attention_probs = probs
+        blk.multi_head._probs_skipped = probs is None       # a later read warns once (transformer.py)
+        # rows of the post-attention part: all M, or (last block, pruned) the B token-0 rows b*T
+        R, rs = (B, T) if pr else (M, 1)
+        pm = _ops.mask4_empty(R, D, dev) if keep_masks else None      # proj dropout keep bits
+        fm = _ops.mask4_empty(R, D, dev) if keep_masks else None      # fc2 dropout keep bits
+        x_mid = torch.empty(R, D, dtype=dt, device=dev)
+        mk("gemm_fwd", 0, 2.0 * R * D * D, (3 * R * D + D * D) * es)
+        self._gemm_rows(pr, o, self.ww[f"{l}.proj_w"], x_mid, R, D, D, rs * D, D, D, bias=prm[f"{l}.proj_b"],
+                        res=x_in, ldres=rs * D, dropout_p=drop_p, seed=site_seed(seed, l, 0),
+                        drop_row_stride=rs, mask_out=pm)
+        mk("gemm_fwd", 1)
+        mk("ln_fwd", 0, 0.0, 2 * R * D * es + 8 * R)
+        a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
+        mk("ln_fwd", 1)
+        # saved for the backward: the ReLU mask as 1 bit per element (mask4, read by fc2's dgrad epilogue instead
+        # of re-reading h: 1/16 of the bytes)
+        hm = _ops.mask4_empty(R, 4 * D, dev) if save else None
+        mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + (R * D // 2 if save else 0))
+        h = torch.empty(R, 4 * D, dtype=dt, device=dev)
+        self._gemm_rows(pr, a2, self.ww[f"{l}.fc1_w"], h, R, 4 * D, D, D, D, 4 * D, bias=prm[f"{l}.fc1_b"],
+                        act=ACT_RELU, mask_out=hm)
+        mk("gemm_fwd", 1)
+        x_out = torch.empty(R, D, dtype=dt, device=dev)
+        mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + 2 * R * D) * es)
+        self._gemm_rows(pr, h, self.ww[f"{l}.fc2_w"], x_out, R, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
+                        res=x_mid, ldres=D, dropout_p=drop_p, seed=site_seed(seed, l, 1), drop_row_stride=rs,
+                        mask_out=fm)
+        mk("gemm_fwd", 1)
+        saved = (x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm) if save else None
+        return x_out, saved
 
     # ------------------------------------------------------------------------------------------------------------
     # backward
@@ -560,12 +574,10 @@ class Engine:
         return self._comm_events[0].elapsed_time(self._comm_events[1])
 
     def backward(self, tape, dlogits):
-        D, T, N, H, hd, L, dt = self.D, self.T, self.N, self.H, self.hd, self.L, self.dtype
+        D, T, N, L, dt = self.D, self.T, self.N, self.L, self.dtype
         B = tape.B
         M = B * T
         prm, gw = self.params, self.gw
-        es = 2 if dt == torch.bfloat16 else 4
-        mk = self._mark
         # decided at backward time: the reference calls zero_grad(set_to_none=True) between forward and backward
         beta = self._attach_grads()
         # Accumulating into existing .grad (no zero_grad between backwards) with `register_hook` hooks present:
@@ -580,10 +592,11 @@ class Engine:
         req = {k: any(p.requires_grad for p in ps) for k, ps in self.owners.items()}
         # a frozen per-head parameter whose .grad is still a view of G shares the fused QKV gradient region with the
         # heads that do train; that region is rewritten as a whole, so keep the frozen view's value aside (autograd
-        # leaves a frozen parameter's .grad untouched)
-        self._frozen_keep = [(gv, gv.clone()) for p, gv in self.grad_views
-                             if not p.requires_grad and p.grad is not None and p.grad.data_ptr() == gv.data_ptr()
-                             and self._acc_old is None]
+        # leaves a frozen parameter's .grad untouched).  Only such views: a region whose owners are all frozen is
+        # never written.
+        self._frozen_keep = [] if self._acc_old is not None else [
+            (gv, gv.clone()) for (p, gv), key in zip(self.grad_views, self.grad_region)
+            if not p.requires_grad and req[key] and p.grad is not None and p.grad.data_ptr() == gv.data_ptr()]
         # the backward stops at the first block below which nothing (parameters, input image) needs a gradient
         below = tape.x_grad or any(req[k] for k in ("conv_w", "conv_b", "cls", "pos"))
         need_from = {}
@@ -624,8 +637,7 @@ class Engine:
         _ops.copy2d(dz, D, dx, D if pruned else T * D, B, D)
         # Dropout backward as a bare mask (exact in bf16); its 1/(1-p) goes into every consumer of the masked gradient
         # (GEMM alpha, column-sum alpha, the LN kernels' bias-gradient sums) instead of a rounding of its own.  The
-        # keep bits are the ones the forward's GEMM epilogues saved (mask4), not a re-hash.
-        gs = 1.0 / (1.0 - DROPOUT_P) if tape.training else 1.0
+        # keep bits are the ones the forward's GEMM epilogues saved (mask4), not a re-hash (block_backward).
         if tape.training:
             g1 = _ops.mask4_apply(dx, torch.empty_like(dx), tape.blocks[L - 1][15], 1.0)
         else:
@@ -635,89 +647,12 @@ class Engine:
         for l in reversed(range(L)):
             if not need_from[l]:
                 break
-            x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm = tape.blocks[l]
-            pr = pruned and l == L - 1
-            R, rs = (B, T) if pr else (M, 1)
-            # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
-            if req[f"{l}.fc2_w"]:
-                self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, R, D, 4 * D, beta, side, "gemm_wgrad", alpha=gs)
-            if not g1_summed:
-                self._colsum(g1, R, D, D, gw[f"{l}.fc2_b"], beta, alpha=gs)
-            dh = torch.empty(R, 4 * D, dtype=dt, device=dev)
-            dh_part = torch.empty(_ops.colsum_part_rows(R), 4 * D, dtype=torch.float32, device=dev)
-            # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
-            mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + R * D // 2)
-            self._gemm_rows(pr, g1, self.ww[f"{l}.fc2_w"], dh, R, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
-                            colsum_part=dh_part, alpha=gs, shared_cus=self.shared_cus)
-            mk("gemm_dgrad", 1)
-            cs_jobs = [(dh_part, [gw[f"{l}.fc1_b"]], beta)]      # this block's bias / LN-affine sums: one launch below
-            if req[f"{l}.fc1_w"]:
-                self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, R, 4 * D, D, beta, side, "gemm_wgrad")
-            da2 = torch.empty(R, D, dtype=dt, device=dev)
-            mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + R * D) * es)
-            self._gemm_rows(pr, dh, self.ww[f"{l}.fc1_w"], da2, R, D, 4 * D, 4 * D, D, D, b_kcontig=False,
-                            shared_cus=self.shared_cus)
-            mk("gemm_dgrad", 1)
-            dx_mid = torch.empty(R, D, dtype=dt, device=dev)
-            g0 = torch.empty(R, D, dtype=dt, device=dev) if tape.training else None
-            # ln2 backward + residual add + dropout backward of the MHA branch; its third partial set is the column
-            # sums of g0 as stored = the proj bias gradient
-            mk("ln_bwd", 0, 0.0, (3 + 1 + (g0 is not None)) * R * D * es + 8 * R + R * D // 8)
-            part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx, drop_out=g0,
-                                      drop_p=DROPOUT_P, drop_mask=pm, osum=True)
-            mk("ln_bwd", 1)
-            cs_jobs.append((part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta))
-            if g0 is None:
-                g0 = dx_mid
-            # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
-            if req[f"{l}.proj_w"]:
-                self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, R, D, rs * D, beta, side, "gemm_wgrad", alpha=gs)
-            do = torch.empty(R, D, dtype=dt, device=dev)
-            mk("gemm_dgrad", 0, 2.0 * R * D * D, (2 * R * D + D * D) * es)
-            self._gemm_rows(pr, g0, self.ww[f"{l}.proj_w"], do, R, D, D, D, D, D, b_kcontig=False, alpha=gs,
-                            shared_cus=self.shared_cus)
-            mk("gemm_dgrad", 1)
-            if pr:
-                # back to all M rows for the attention backward (zero outside the token-0 rows)
-                do_full = torch.zeros(M, D, dtype=dt, device=dev)
-                _ops.copy2d(do, D, do_full, T * D, B, D)
-                dxm_full = torch.zeros(M, D, dtype=dt, device=dev)
-                _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
-                do, dx_mid = do_full, dxm_full
-            if o32 is None and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
-                # the forward chose the fused backward (no fp32 O kept) and a library option changed since: the tiled
-                # backward would form delta from the bf16 O, inexact under saturated softmax
-                raise RuntimeError("attention backward needs the fp32 O that this forward did not keep: the "
-                                   "attn_bwd_split library option changed between forward and backward")
-            # bytes: qkv, dO, dqkv (+ O and o32 for the tiled backward's delta pass)
-            mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 7 * M * D * es + 4 * B * H * T + (M * D * es + 4 * M * D if o32
-                                                                                          is not None else 0))
-            dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
-                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32,
-                                 shared_cus=self.shared_cus)
-            mk("attn_bwd", 1)
-            if req[f"{l}.qkv_w"]:
-                self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
-            da1 = torch.empty(M, D, dtype=dt, device=dev)
-            mk("gemm_dgrad", 0, 2.0 * M * 3 * D * D, (3 * M * D + 3 * D * D + M * D) * es)
-            self._gemm_bwd(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
-            mk("gemm_dgrad", 1)
-            dx_in = torch.empty(M, D, dtype=dt, device=dev)
-            g1n = torch.empty(M, D, dtype=dt, device=dev) if (tape.training and l > 0) else None
-            # ln1 backward; for l > 0 its third partial set is the column sums of the next g1 (g1n, or dx_in in eval)
-            # = the fc2 bias gradient of block l-1
-            mk("ln_bwd", 0, 0.0, (3 + 1 + (g1n is not None)) * M * D * es + 8 * M)
-            part = _ops.layernorm_bwd(da1, x_in, prm[f"{l}.ln1_w"], m1, r1, dx_in, dres=dx_mid, drop_out=g1n,
-                                      drop_p=DROPOUT_P, drop_mask=tape.blocks[l - 1][15] if g1n is not None else None,
-                                      osum=l > 0)
-            mk("ln_bwd", 1)
-            outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if l > 0 else [])
-            cs_jobs.append((part, outs, beta))
-            _ops.colsum_finish_batch(cs_jobs)
+            prev_mask = tape.blocks[l - 1][15] if (tape.training and l > 0) else None
+            dx, g1n = self.block_backward(l, tape.blocks[l], dx, g1, g1_summed, beta, req, side, tape.training, B,
+                                          pruned and l == L - 1, chain_prev=l > 0, prev_mask=prev_mask)
             g1_summed = l > 0
             self._bucket_ready(self.block_range[l], side)
-            dx = dx_in
-            g1 = g1n if g1n is not None else dx_in
+            g1 = g1n if g1n is not None else dx
         dimg = None
         if need_from[0]:
             # ---- embedding (vit.py:39-42): dx = d(x0) [B*T, D]
@@ -743,6 +678,102 @@ class Engine:
             torch.cuda.current_stream(dev).wait_stream(side)      # every weight gradient is in G before the step
         self._finish_buckets()
         return dimg
+
+    def block_backward(self, l, saved, dx, g1, g1_summed, beta, req, side, training, B, pr=False, chain_prev=False,
+                       prev_mask=None):
+        """Backward of block l from d(x_out) = dx and g1 = the fc2-dropout-masked dx (dx itself in eval).  Writes the
+        block's weight gradients into the flat buffer (beta: 0 overwrite / 1 accumulate; req: which regions want a
+        gradient) and returns (dx_in, g1n).  `chain_prev`: there is a block l-1 below, so the ln1 backward also emits
+        block l-1's fc2 bias-gradient column sums and — in training, from its keep bits `prev_mask` — g1n, the next
+        block's masked gradient (None otherwise).  `g1_summed`: this block's fc2 bias gradient was already summed by
+        the block above.  `pr`: the pruned last block (dx / g1 are its B token-0 rows)."""
+        D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
+        M = B * T
+        gw = self.gw
+        prm = self.params
+        es = 2 if dt == torch.bfloat16 else 4
+        mk = self._mark
+        dev = dx.device
+        gs = 1.0 / (1.0 - DROPOUT_P) if training else 1.0
+        R, rs = (B, T) if pr else (M, 1)
+        x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm = saved
+        # FFN: x_out = x_mid + drop(relu(ln2(x_mid) W1^T + b1) W2^T + b2)
+        if req[f"{l}.fc2_w"]:
+            self._wgrad(g1, h, gw[f"{l}.fc2_w"], D, 4 * D, R, D, 4 * D, beta, side, "gemm_wgrad", alpha=gs)
+        if not g1_summed:
+            self._colsum(g1, R, D, D, gw[f"{l}.fc2_b"], beta, alpha=gs)
+        dh = torch.empty(R, 4 * D, dtype=dt, device=dev)
+        dh_part = torch.empty(_ops.colsum_part_rows(R), 4 * D, dtype=torch.float32, device=dev)
+        # relu backward and the fc1 bias-gradient column sums fused into the dgrad epilogue
+        mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + R * D // 2)
+        self._gemm_rows(pr, g1, self.ww[f"{l}.fc2_w"], dh, R, 4 * D, D, D, 4 * D, 4 * D, b_kcontig=False, aux=hm,
+                        colsum_part=dh_part, alpha=gs, shared_cus=self.shared_cus)
+        mk("gemm_dgrad", 1)
+        cs_jobs = [(dh_part, [gw[f"{l}.fc1_b"]], beta)]      # this block's bias / LN-affine sums: one launch below
+        if req[f"{l}.fc1_w"]:
+            self._wgrad(dh, a2, gw[f"{l}.fc1_w"], 4 * D, D, R, 4 * D, D, beta, side, "gemm_wgrad")
+        da2 = torch.empty(R, D, dtype=dt, device=dev)
+        mk("gemm_dgrad", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + R * D) * es)
+        self._gemm_rows(pr, dh, self.ww[f"{l}.fc1_w"], da2, R, D, 4 * D, 4 * D, D, D, b_kcontig=False,
+                        shared_cus=self.shared_cus)
+        mk("gemm_dgrad", 1)
+        dx_mid = torch.empty(R, D, dtype=dt, device=dev)
+        g0 = torch.empty(R, D, dtype=dt, device=dev) if training else None
+        # ln2 backward + residual add + dropout backward of the MHA branch; its third partial set is the column
+        # sums of g0 as stored = the proj bias gradient
+        mk("ln_bwd", 0, 0.0, (3 + 1 + (g0 is not None)) * R * D * es + 8 * R + R * D // 8)
+        part = _ops.layernorm_bwd(da2, x_mid, prm[f"{l}.ln2_w"], m2, r2, dx_mid, dres=dx, drop_out=g0,
+                                  drop_p=DROPOUT_P, drop_mask=pm, osum=True)
+        mk("ln_bwd", 1)
+        cs_jobs.append((part, [gw[f"{l}.ln2_w"], gw[f"{l}.ln2_b"], gw[f"{l}.proj_b"]], beta))
+        if g0 is None:
+            g0 = dx_mid
+        # MHA: x_mid = x_in + drop(attn(ln1(x_in)) Wp^T + bp)
+        if req[f"{l}.proj_w"]:
+            self._wgrad(g0, o, gw[f"{l}.proj_w"], D, D, R, D, rs * D, beta, side, "gemm_wgrad", alpha=gs)
+        do = torch.empty(R, D, dtype=dt, device=dev)
+        mk("gemm_dgrad", 0, 2.0 * R * D * D, (2 * R * D + D * D) * es)
+        self._gemm_rows(pr, g0, self.ww[f"{l}.proj_w"], do, R, D, D, D, D, D, b_kcontig=False, alpha=gs,
+                        shared_cus=self.shared_cus)
+        mk("gemm_dgrad", 1)
+        if pr:
+            # back to all M rows for the attention backward (zero outside the token-0 rows)
+            do_full = torch.zeros(M, D, dtype=dt, device=dev)
+            _ops.copy2d(do, D, do_full, T * D, B, D)
+            dxm_full = torch.zeros(M, D, dtype=dt, device=dev)
+            _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
+            do, dx_mid = do_full, dxm_full
+        if o32 is None and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
+            # the forward chose the fused backward (no fp32 O kept) and a library option changed since: the tiled
+            # backward would form delta from the bf16 O, inexact under saturated softmax (ADVICE r3)
+            raise RuntimeError("attention backward needs the fp32 O that this forward did not keep: the "
+                               "attn_bwd_split library option changed between forward and backward")
+        # bytes: qkv, dO, dqkv (+ O and o32 for the tiled backward's delta pass)
+        mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 7 * M * D * es + 4 * B * H * T + (M * D * es + 4 * M * D if o32
+                                                                                      is not None else 0))
+        dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
+                             workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32,
+                             shared_cus=self.shared_cus)
+        mk("attn_bwd", 1)
+        if req[f"{l}.qkv_w"]:
+            self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
+        da1 = torch.empty(M, D, dtype=dt, device=dev)
+        mk("gemm_dgrad", 0, 2.0 * M * 3 * D * D, (3 * M * D + 3 * D * D + M * D) * es)
+        self._gemm_bwd(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
+        mk("gemm_dgrad", 1)
+        dx_in = torch.empty(M, D, dtype=dt, device=dev)
+        g1n = torch.empty(M, D, dtype=dt, device=dev) if (training and chain_prev) else None
+        # ln1 backward; for l > 0 its third partial set is the column sums of the next g1 (g1n, or dx_in in eval)
+        # = the fc2 bias gradient of block l-1
+        mk("ln_bwd", 0, 0.0, (3 + 1 + (g1n is not None)) * M * D * es + 8 * M)
+        part = _ops.layernorm_bwd(da1, x_in, prm[f"{l}.ln1_w"], m1, r1, dx_in, dres=dx_mid, drop_out=g1n,
+                                  drop_p=DROPOUT_P, drop_mask=prev_mask if g1n is not None else None,
+                                  osum=chain_prev)
+        mk("ln_bwd", 1)
+        outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if chain_prev else [])
+        cs_jobs.append((part, outs, beta))
+        _ops.colsum_finish_batch(cs_jobs)
+        return dx_in, g1n
 
     def run_param_hooks(self):
         """Parameter hooks after the fused backward (autograd's AccumulateGrad never runs for these parameters):

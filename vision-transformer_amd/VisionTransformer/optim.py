@@ -24,8 +24,9 @@ class FusedAdamW(torch.optim.Optimizer):
     `.item()` or `+= 1` on the step path.  Device chunk tables are cached per (group, step-count class) and hold
     references to every tensor whose pointer they carry.  A cached table is reused while the optimizer's version
     (bumped by load_state_dict / add_param_group / fresh state) is unchanged and every parameter still has the very
-    same .grad tensor object and every tabled tensor (parameter, gradient, moments) still has the storage it was
-    tabled with, so `p.data = other` or a replaced moment tensor rebuilds the table by itself."""
+    same .grad tensor object, the same moment tensor objects and every parameter the storage it was tabled with, so
+    `p.data = other` or a replaced moment tensor rebuilds the table by itself (one data_ptr() per parameter per step,
+    no per-step pointer signature of gradients and moments)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, grad_scale=1.0):
         if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
@@ -121,30 +122,31 @@ class FusedAdamW(torch.optim.Optimizer):
                     dev_tab, n = _ops.build_chunk_table(entries, ps[0].device)
                     # entries keep every tabled tensor alive; the raw shadow list is what the identity check compares
                     tab = (self._version, list(ps), [p.grad for p in ps], [shadow_of(p) for p in ps], dev_tab, n,
-                           sdt, entries, self._pointer_sig(ps))
+                           sdt, entries, [p.data_ptr() for p in ps],
+                           [(self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"]) for p in ps])
                     self._tables[key] = tab
                 dev_tab, n, sdt = tab[4], tab[5], tab[6]
                 _ops.adamw(dev_tab, n, group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** t,
                            1.0 - b2 ** t, self.grad_scale, sdt)
         return loss
 
-    def _pointer_sig(self, ps):
-        """Storage of every tabled tensor: parameter, gradient and both moments (`p.data = ...` or a
-        replaced `state[p]['exp_avg']` re-points storage without any object identity changing)."""
-        out = []
-        for p in ps:
-            st = self.state[p]
-            out += [p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()]
-        return out
-
     def _table_valid(self, tab, ps):
-        """Same optimizer version, same parameters, every parameter still holds the same .grad tensor object as when
-        the table was built, and no tabled tensor's storage moved (parameter, gradient, moments).  The engine's
-        shadows change only when it rebuilds its buffers, and then every gradient view is a new object too."""
-        ver, tps, grads = tab[0], tab[1], tab[2]
-        return (ver == self._version and len(tps) == len(ps)
-                and all(a is b and a.grad is g for a, b, g in zip(tps, ps, grads))
-                and self._pointer_sig(ps) == tab[8])
+        """Same optimizer version, same parameters, every parameter still holds the same .grad tensor object and the
+        same moment tensor objects as when the table was built, and no parameter's storage moved (`p.data = ...`
+        re-points storage without changing any object identity).  One data_ptr() per parameter plus
+        identity checks: this runs every step.  The engine's shadows change only when it rebuilds its buffers, and
+        then every gradient view is a new object too."""
+        ver, tps, grads, ptrs, moments = tab[0], tab[1], tab[2], tab[8], tab[9]
+        if ver != self._version or len(tps) != len(ps):
+            return False
+        state = self.state
+        for a, b, g, ptr, (m, v) in zip(tps, ps, grads, ptrs, moments):
+            if a is not b or a.grad is not g or a.data_ptr() != ptr:
+                return False
+            st = state[a]
+            if st["exp_avg"] is not m or st["exp_avg_sq"] is not v:
+                return False
+        return True
 
 
 class _XentFn(torch.autograd.Function):

@@ -101,8 +101,10 @@ class VisionTransformer(nn.Module):
         `grad_dtype=torch.bfloat16` sends each bucket as bf16 (half the xGMI ring bytes): the fp32 gradients are
         rounded to bf16, averaged in bf16 and widened back; master weights and optimizer state stay fp32.
         `launch_mode` of the backward's GEMMs and fused attention backward beside the collectives: "shared" (one
-        workgroup per item, VIT_FLAG_SHARED_CUS), "persistent" (one workgroup per CU) or "auto" (shared on nccl,
-        where RCCL's kernels hold CUs).  Results are bitwise the same in every mode."""
+        workgroup per item, VIT_FLAG_SHARED_CUS), "persistent" (one workgroup per CU) or "auto" = persistent: with
+        CU-holding kernels beside the backward in place of RCCL's (tools/cu_hog_ab.py) the persistent grids stayed
+        0.2-0.3 ms/step faster than the shared-CU launch, whose own cost is 0.4-0.7 ms/step (no N > 1
+        measurement exists yet).  Results are bitwise the same in every mode."""
         import torch.distributed as dist
         if not dist.is_initialized():
             raise RuntimeError("enable_data_parallel: torch.distributed is not initialised")
@@ -114,12 +116,9 @@ class VisionTransformer(nn.Module):
         eng.ddp_group = group
         eng.comm_dtype = grad_dtype
         eng.ddp_enabled = bool(force) or dist.get_world_size(group) > 1
-        # RCCL's all-reduce kernels run on the GPU beside the backward: by default the backward's kernels then launch
-        # one workgroup per item instead of a persistent one-per-CU grid (VIT_FLAG_SHARED_CUS, vit_hip.h)
-        if launch_mode == "auto":
-            eng.shared_cus = eng.ddp_enabled and dist.get_backend(group) == "nccl"
-        else:
-            eng.shared_cus = eng.ddp_enabled and launch_mode == "shared"
+        # "shared": the backward's kernels launch one workgroup per item instead of a persistent one-per-CU grid
+        # (VIT_FLAG_SHARED_CUS, vit_hip.h), so RCCL's all-reduce kernels beside them never wait for a whole grid
+        eng.shared_cus = eng.ddp_enabled and launch_mode == "shared"
         return self
 
     # the engine holds a weakref to its model and views of the parameters: never copy or pickle it (a deep copy or

@@ -55,34 +55,83 @@ def _writer(log_dir):
         return _JsonlWriter(log_dir)
 
 
+class ShardSampler(torch.utils.data.Sampler):
+    """Rank `rank` of `world` reads indices rank, rank + world, ... < n in order: the shards partition the set exactly
+    (DistributedSampler instead pads every shard to equal length with duplicates), so a sharded evaluate() scores
+    every test sample once."""
+
+    def __init__(self, dataset, rank=None, world=None):
+        r, w = _rank_world()
+        self.n = len(dataset)
+        self.rank = r if rank is None else rank
+        self.world = w if world is None else world
+
+    def __iter__(self):
+        return iter(range(self.rank, self.n, self.world))
+
+    def __len__(self):
+        return len(range(self.rank, self.n, self.world))
+
+
+def _sampler_of(loader):
+    for obj in (loader, getattr(loader, "loader", None)):
+        if obj is None:
+            continue
+        for s in (getattr(obj, "sampler", None), getattr(getattr(obj, "batch_sampler", None), "sampler", None)):
+            if isinstance(s, (torch.utils.data.DistributedSampler, ShardSampler)):
+                return s
+    return None
+
+
 @torch.no_grad()
 def evaluate(model, test_loader, eval_func, avg=None):
     """Mean over batches of eval_func(labels, argmax(logits)) (train.py:29-44).
 
-    Under data parallelism (an initialized process group of world size > 1) every rank scores the batches of its
-    own shard of the test set and the (score sum, batch count) pair is all-reduced, so every rank returns the mean
-    over all ranks' batches — with equal batches (drop_last), the accuracy over the whole test set."""
+    A partial last batch is padded to the model's batch size (the CLS parameter is batch-shaped, vit.py:32,41) and
+    only its real rows are scored; the reference would raise there.
+
+    Under data parallelism (an initialized process group of world size > 1) every rank scores its own shard of the test
+    set, the (label, prediction) pairs of all ranks are gathered, and eval_func runs once over the whole set, so every
+    rank returns the same score — for accuracy, the exact whole-set accuracy.  Each sample counts once: a ShardSampler
+    shard has no duplicates, and the padding duplicates DistributedSampler appends (the trailing samples of a shard
+    whose global position is >= len(dataset)) are dropped."""
     model.eval()
     score = 0.0
     n = 0
+    labs, preds = [], []
+    pad_to = getattr(getattr(model, "vit_config", None), "batch_size", None)
     for tensors, labels in test_loader:
-        logits = model(tensors.to(device, non_blocking=True))
+        rows = tensors.shape[0]
+        if pad_to is not None and rows < pad_to:
+            fill = tensors[-1:].expand(pad_to - rows, *tensors.shape[1:])
+            tensors = torch.cat([tensors, fill], 0)
+        logits = model(tensors.to(device, non_blocking=True))[:rows]
         predictions = torch.argmax(logits, axis=-1).to("cpu")
         labels = labels.to("cpu")
+        labs.append(labels)
+        preds.append(predictions)
         if avg is None:
             score += eval_func(labels, predictions)
         else:
             score += eval_func(labels, predictions, average=avg, zero_division=0.0)
         n += 1
     model.train()
-    _, world = _rank_world()
-    if world > 1:
-        on_dev = dist.get_backend() == "nccl"
-        t = torch.tensor([float(score), float(n)], dtype=torch.float64,
-                         device=torch.device("cuda", torch.cuda.current_device()) if on_dev else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        score, n = float(t[0]), int(t[1])
-    return score / max(n, 1)
+    rank, world = _rank_world()
+    if world == 1:
+        return score / max(n, 1)
+    lab = torch.cat(labs) if labs else torch.zeros(0, dtype=torch.long)
+    pred = torch.cat(preds) if preds else torch.zeros(0, dtype=torch.long)
+    s = _sampler_of(test_loader)
+    if isinstance(s, torch.utils.data.DistributedSampler) and not s.drop_last:
+        keep = len(range(rank, len(s.dataset), world))           # the shard's samples before the padding
+        lab, pred = lab[:keep], pred[:keep]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (lab.tolist(), pred.tolist()))
+    all_lab = torch.tensor([v for g in gathered for v in g[0]], dtype=torch.long)
+    all_pred = torch.tensor([v for g in gathered for v in g[1]], dtype=torch.long)
+    if avg is None:
+        return float(eval_func(all_lab, all_pred))
+    return float(eval_func(all_lab, all_pred, average=avg, zero_division=0.0))
 
 
 def _set_epoch(loader, epoch):
@@ -315,15 +364,16 @@ def main():
             train_set = D.SyntheticRawImages(args.train_size, (32, 32, 3), args.classes, seed=1 + rank)
             test_set = D.SyntheticRawImages(args.test_size, (32, 32, 3), args.classes, seed=10_000)
     sampler = torch.utils.data.DistributedSampler(train_set) if world > 1 else None
-    # the test set is sharded too; evaluate() all-reduces the counts
-    tsampler = torch.utils.data.DistributedSampler(test_set, shuffle=False) if world > 1 else None
+    # the test set is sharded too (each sample on exactly one rank); evaluate() gathers the predictions
+    tsampler = ShardSampler(test_set) if world > 1 else None
     if args.data != "synthetic" and device == "cuda":
         from VisionTransformer import data as D
         # one transform (and coefficient workspace) per loader: each stages its batches on its own side stream
         train_loader = D.DeviceBatches(D.raw_loader(train_set, args.batch, shuffle=True, num_workers=args.workers,
                                                     sampler=sampler), D.GpuImageTransform(args.img), device)
         test_loader = D.DeviceBatches(D.raw_loader(test_set, args.batch, shuffle=False, num_workers=args.workers,
-                                                   sampler=tsampler), D.GpuImageTransform(args.img), device)
+                                                   drop_last=False, sampler=tsampler), D.GpuImageTransform(args.img),
+                                      device)
     else:
         if args.data != "synthetic":
             from VisionTransformer import data as D
@@ -331,8 +381,9 @@ def main():
         train_loader = torch.utils.data.DataLoader(train_set, batch_size=args.batch, shuffle=sampler is None,
                                                    sampler=sampler, num_workers=args.workers, drop_last=True,
                                                    pin_memory=pin)
+        # a partial last test batch is padded by evaluate() (the CLS parameter is batch-shaped)
         test_loader = torch.utils.data.DataLoader(test_set, batch_size=args.batch, num_workers=args.workers,
-                                                  sampler=tsampler, drop_last=True, pin_memory=pin)
+                                                  sampler=tsampler, drop_last=False, pin_memory=pin)
     train(cfg, train_loader, test_loader, args.epochs, args.eval_iter, args.log_dir, args.checkpoint_dir,
           lr=args.lr, max_steps=args.steps, reference_loop=args.reference_loop)
     if world > 1:
