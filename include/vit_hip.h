@@ -60,6 +60,7 @@ const char* vit_last_error(void);
  *   "attn_bwd_grid"      0 (automatic): workgroups of the persistent attention backward
  *   "ln16"               1: the 16-B-per-lane LayerNorm forward where the layout allows it
  *   "ln_al"              1: LayerNorm backward accumulators in LDS (0: registers)
+ *   "attn_fwd_ring"      1: the persistent ring attention forward for T <= 256 (0: one workgroup per (image, head))
  * vit_set_option returns VIT_ERR_INVALID for an unknown name; vit_get_option returns INT64_MIN for one. */
 int vit_set_option(const char* name, int64_t value);
 int64_t vit_get_option(const char* name);

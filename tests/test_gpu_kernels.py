@@ -445,11 +445,13 @@ def _attn_flash_grads(qkv, d_o, B, T, H, hd, scale):
 
 
 def _check_attn_bwd_bf16(dqkv, ref, D, tol=2e-2):
-    """Norm-wise error of each of dQ, dK, dV against the same-rounding reference."""
+    """Norm-wise error of each of dQ, dK, dV against the same-rounding reference (relative to the larger of its own
+    norm and 1e-3 of the whole gradient's)."""
     errs = {}
+    floor = 1e-3 * float(ref.norm())            # T = 1: dQ = dK = 0 exactly (one key), the kernels leave ~1e-6
     for name, sl in (("dQ", slice(0, D)), ("dK", slice(D, 2 * D)), ("dV", slice(2 * D, 3 * D))):
         a, r = dqkv[:, sl].double(), ref[:, sl]
-        errs[name] = float((a - r).norm() / max(float(r.norm()), 1e-30))
+        errs[name] = float((a - r).norm() / max(float(r.norm()), floor, 1e-30))
     print("attention backward vs same-rounding fp64:", {k: f"{v:.2e}" for k, v in errs.items()})
     assert all(e <= tol for e in errs.values()), errs
 

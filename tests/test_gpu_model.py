@@ -396,14 +396,44 @@ def test_full_size_configs_properties(preset, img, batch):
     assert losses[2] < losses[0], losses
 
 
+def _engine_relu_masks(m, x, L, B, T, D, own):
+    """The engine's ReLU branch decisions per block (the forward's saved mask4 bits, decoded by vit_mask4_apply) as
+    bool [B, T, 4D]; the pruned last block has them for its token-0 rows only, its other rows keep `own` (the oracle's
+    decisions: those rows carry no gradient and are never read)."""
+    _, tape = m.hip_engine.forward(x, False, True)
+    out = {}
+    for l in range(L):
+        hm = tape.blocks[l][13]
+        R = B if (tape.pruned and l == L - 1) else B * T
+        ones = torch.ones(R, 4 * D, device=DEV)
+        bits = _ops.mask4_apply(ones, torch.empty_like(ones), hm, 1.0) > 0
+        if R == B * T:
+            out[l] = bits.view(B, T, 4 * D)
+        else:
+            full = own[l].clone()
+            full[:, 0] = bits
+            out[l] = full
+    return out
+
+
 def test_vit_base_full_depth_fp32_vs_fp64():
     """ViT-B/16 at FULL depth (12 blocks, transformer.py:82-90), 224^2, B=8, fp32, eval mode, through the engine vs the
-    oracle evaluated on the GPU in fp64.  Gates: logits max-abs error vs fp64 <=
-    max(1e-4, 2x the fp32 oracle's (torch GEMMs: what the reference runs) error vs fp64); every gradient per tensor
-    within max(2e-4, 8x the larger error of two valid fp32 summation orders — the torch one and the oracle with
-    sequential-chain accumulation, this path's order) vs fp64, and the whole gradient vector within 2x the
-    sequential-order sample (the rule of test_tiny_c1_fp32_vs_reference)."""
+    oracle evaluated on the GPU in fp64.  Gates:
+      * logits: max-abs error vs fp64 <= max(1e-4, 2x the fp32 oracle's error vs fp64 (torch GEMMs: what the
+        reference runs));
+      * ReLU branches: the FFN ReLU decides on the sign of a pre-activation, and one whose value sits at 0 to within
+        rounding can go either way in any valid evaluation; with few gradient rows (the pruned last block: B token-0
+        rows, 24.6k hidden values) one such flip moves that block's fc1 / ln2 gradients by ~1% (measured: 0.9%; the
+        teacher-forced fp32 blocks show the same 1e-3 jumps at blocks where a flip occurs).  So every engine decision
+        that differs from fp64's must be a near-tie (|pre-activation| <= 1e-3 of its row's max: at depth the block
+        inputs themselves carry the amplified rounding of the blocks below), and such flips must be rare (<= 1e-5 of
+        the decisions; a wrong mask bit layout flips ~half of them); then
+      * gradients vs fp64 evaluated with the engine's ReLU branches (the way the dropout masks are shared): every
+        tensor within max(2e-4, 8x the larger error of two valid fp32 summation orders — torch's and the oracle with
+        sequential-chain accumulation, this path's order — on the same branches), and the whole gradient vector
+        within 2x the sequential-order sample (the rule of test_tiny_c1_fp32_vs_reference)."""
     ocfg = O.make_config("base", img=224, batch=8, num_classes=1000)
+    L, B, T, D = ocfg.num_blocks, ocfg.batch_size, ocfg.T, ocfg.embedding_size
     st = O.init_state(ocfg, seed=31)
     m = _model(ocfg)
     m.load_state_dict(st)
@@ -414,17 +444,34 @@ def test_vit_base_full_depth_fp32_vs_fp64():
     cross_entropy(logits, yd).backward()
     ours = {k: p.grad.detach().double() for k, p in m.named_parameters()}
     logits = logits.detach().double()
+    sd = {k: v.to(DEV) for k, v in st.items()}
+    pre64 = {}
+    lg64, _, g64_own = O.loss_and_grads(sd, xd, yd, ocfg, dtype=torch.float64, record=pre64)
+    own = {l: pre64[l] > 0 for l in range(L)}
+    with torch.no_grad():
+        masks = _engine_relu_masks(m, xd, L, B, T, D, own)
     del m
     torch.cuda.empty_cache()
-    sd = {k: v.to(DEV) for k, v in st.items()}
-    lg32, _, g32 = O.loss_and_grads(sd, xd, yd, ocfg)
-    lg64, _, g64 = O.loss_and_grads(sd, xd, yd, ocfg, dtype=torch.float64)
-    lgsq, _, gsq = O.loss_and_grads(sd, xd, yd, ocfg, seq_chain=True)
+    lg32, _, _ = O.loss_and_grads(sd, xd, yd, ocfg)
     ref_err = float((lg32.double() - lg64).abs().max())
-    seq_err = float((lgsq.double() - lg64).abs().max())
     our_err = float((logits - lg64).abs().max())
-    print(f"logits max-abs vs fp64: ours {our_err:.3e}, oracle fp32 {ref_err:.3e}, seq-chain {seq_err:.3e}")
+    print(f"logits max-abs vs fp64: ours {our_err:.3e}, oracle fp32 {ref_err:.3e}")
     assert our_err <= max(1e-4, 2 * ref_err), (our_err, ref_err)
+    flips, worst_tie, total = 0, 0.0, 0
+    for l in range(L):
+        rows = slice(None) if l < L - 1 else slice(0, 1)                 # the pruned block decides token 0 only
+        z, mk = pre64[l][:, rows], masks[l][:, rows]
+        diff = mk != (z > 0)
+        total += diff.numel()
+        if bool(diff.any()):
+            scale = z.abs().amax(-1, keepdim=True).expand_as(z)
+            flips += int(diff.sum())
+            worst_tie = max(worst_tie, float((z.abs() / scale)[diff].max()))
+    print(f"ReLU branches differing from fp64: {flips} of {total}, largest |pre-activation| / row max {worst_tie:.2e}")
+    assert worst_tie <= 1e-3 and flips <= max(2, 1e-5 * total), (flips, worst_tie)
+    _, _, g64 = O.loss_and_grads(sd, xd, yd, ocfg, dtype=torch.float64, relu_masks=masks)
+    _, _, g32 = O.loss_and_grads(sd, xd, yd, ocfg, relu_masks=masks)
+    _, _, gsq = O.loss_and_grads(sd, xd, yd, ocfg, seq_chain=True, relu_masks=masks)
     worst, bad = [], []
     cat = {"ours": [], "seq": [], "r64": []}
     for k in g64:
@@ -433,13 +480,15 @@ def test_vit_base_full_depth_fp32_vs_fp64():
         e_ours = float((ours[k].reshape(-1) - r64).norm()) / n64
         e_ref = max(float((g32[k].double().reshape(-1) - r64).norm()),
                     float((gsq[k].double().reshape(-1) - r64).norm())) / n64
-        worst.append((e_ours / max(e_ref, 1e-12), k, e_ours, e_ref))
+        e_own = float((ours[k].reshape(-1) - g64_own[k].reshape(-1)).norm()) / n64
+        worst.append((e_ours / max(e_ref, 1e-12), k, e_ours, e_ref, e_own))
         if e_ours > max(2e-4, 8 * e_ref):
             bad.append((k, e_ours, e_ref))
         cat["ours"].append(ours[k].reshape(-1))
         cat["seq"].append(gsq[k].double().reshape(-1))
         cat["r64"].append(r64)
-    print("worst gradient error ratios (ours / valid-order error):", sorted(worst)[-4:])
+    print("worst gradient error ratios (ours / valid-order error, ours vs fp64 on the same ReLU branches, ours vs "
+          "fp64 on its own branches):", sorted(worst)[-4:])
     assert not bad, bad
     o, sq, r = (torch.cat(cat[n_]) for n_ in ("ours", "seq", "r64"))
     e_all, e_sq = float((o - r).norm()), float((sq - r).norm())

@@ -42,7 +42,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--T", type=int, default=197, help="tokens (577 = 384^2 / patch 16 + cls: the tiled kernels)")
     ap.add_argument("--H", type=int, default=12)
+    ap.add_argument("--opt", action="append", default=[], help="library option name=value (A/B runs)")
     args = ap.parse_args()
+    for kv in args.opt:
+        name, val = kv.split("=")
+        _lib.load().vit_set_option(name.encode(), int(val))
+        print(f"option {name} = {val}")
     B, T, H, hd = args.batch, args.T, args.H, 64
     D = H * hd
     scale = 8.0

@@ -1276,6 +1276,207 @@ __global__ __launch_bounds__(NKB * 64) void attn_fwd_fused(const bf16_t* __restr
   fwd_queries<NKB>(Ks, Vs, qf, wave, lane, Tn, scale * LOG2E, o, o32, lse, b, h, bh, D);
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Ring forward for T <= 256 (round 5; ViT: T = 197): persistent, one workgroup of NT = ceil(T/16) waves per CU, wave w
+// owning queries 16w .. 16w + 15 of every (image, head) item the workgroup takes (items g, g + grid, ...).
+//   * K and V of an item are LDS-DMA'd into a [Tp][64] image pair (Tp = 16 NT: 208 rows at T = 197, 53 KB) of a ring of
+//     NS slots (3 while they fit in the 160 KiB: the item two ahead streams in while this one computes; 2 above
+//     T = 208).  Each wave issues 4 of the item's 4 NT pieces, so HBM sees a continuous stream instead of the burst at
+//     the start of every one-item workgroup.
+//   * Q of the next item is LDS-DMA'd into the K image of the current slot once every wave is past its S products
+//     (2 pieces per wave), and read as MFMA fragments after the next item's first barrier.  Every global load is
+//     LDS-DMA, so the counted `s_waitcnt vmcnt` at the top of an item retires exactly this item's K / V / Q pieces and
+//     leaves the ring's next K / V in flight (a register load would get a compiler wait that drains it).
+//   * Exact two-pass softmax on 16x16x32 MFMAs: S^T = K Q^T for all keys (NT accumulators of 4: one query per lane
+//     column, keys 4g + i of each 16-key tile on lane group g), the row max and sum over a lane's 4 NT values plus two
+//     permlane swaps, P = exp2(S c2 - max c2) in place, then O^T = V^T P^T with P^T as the B operand straight from the
+//     accumulators: the 32 keys of a k-step are keys 4g + 0..3 of tiles (2j, 2j + 1) for lane group g, and the V^T
+//     A operand reads exactly those rows (two ds_read_b64_tr_b16).  No online rescaling, no running max.
+//   * LDS images: 128-B rows, 16-B chunk c of row r at position c ^ (r & 6): conflict-free for the ds_read_b128 K / Q
+//     reads (16 rows x one chunk per 16-lane group) and the transposed V reads (8 rows x 2 chunks per 32-lane half).
+// Numerics as oracle _FlashBF16Attention: unnormalised P rounded to bf16 for P V, normalised by the unrounded sum.
+// ---------------------------------------------------------------------------------------------------------------
+VIT_DEV void ring_piece(const bf16_t* base, int64_t row0, int64_t ld, int64_t col0, int Tn, bf16_t* img, int pc,
+                        int lane) {
+  lane = remat(lane);
+  const int r = pc * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ (r & 6);
+  const bf16_t* src = base + (row0 + min(r, Tn - 1)) * ld + col0 + c * 8;   // rows >= T: finite copies, masked
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(img + pc * 512));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o,
+                                                           float* __restrict__ o32, float* __restrict__ lse,
+                                                           int64_t Tn64, int64_t H, int64_t items, float scale) {
+  constexpr int Tp = NT * 16;
+  constexpr int IMG = Tp * HD;                        // elements of one [Tp][64] image
+  constexpr int SLOT = 2 * IMG;                       // K then V
+  constexpr int NS = 3 * SLOT * 2 <= 160 * 1024 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, ql = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Tn = (int)Tn64;
+  const int64_t D = H * HD, ld = 3 * D;
+  const float c2 = scale * LOG2E;
+  const int q = wave * 16 + ql;                       // this lane's query
+
+  auto kv_item = [&](int64_t it, int slot) {          // this wave's 4 pieces: K and V pieces 2w, 2w + 1
+    const int64_t b = it / H, h = it - (it / H) * H;
+    bf16_t* Ks = smem + slot * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ring_piece(qkv, b * Tn, ld, D + h * HD, Tn, Ks, 2 * wave + i, lane);
+      ring_piece(qkv, b * Tn, ld, 2 * D + h * HD, Tn, Ks + IMG, 2 * wave + i, lane);
+    }
+  };
+  auto q_item = [&](int64_t it, int slot) {           // Q pieces 2w, 2w + 1 into the K image of `slot`
+    const int64_t b = it / H, h = it - (it / H) * H;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ring_piece(qkv, b * Tn, ld, h * HD, Tn, smem + slot * SLOT, 2 * wave + i, lane);
+  };
+
+  int64_t it = blockIdx.x;
+  const int64_t G = gridDim.x;
+  if (it >= items) return;
+  // Every wave issues the same ops in the same order every item — DMA pieces past the last item are issued too, as
+  // harmless re-reads of the last item into slots nothing reads again — because `s_waitcnt vmcnt(N)` retires all but
+  // the N youngest ops: N must never exceed the ops actually issued after the ones it waits for.
+  const auto clampi = [&](int64_t x) { return x < items ? x : items - 1; };
+  // prologue: K/V of the first item (slot 0), its Q (the K image of slot NS - 1), K/V of the second (NS = 3: slot 1)
+  kv_item(it, 0);
+  q_item(it, NS - 1);
+  if (NS == 3) kv_item(clampi(it + G), 1);
+#pragma unroll 1
+  for (int k = 0; it < items; it += G, ++k) {
+    // this item's K / V / Q pieces: the ring's next K / V (4, issued after the 2 Q pieces) and the previous item's 5
+    // stores (4 O + lse: every wave has a valid query row, so none is skipped; 4 more with o32 only make it wait
+    // longer) may stay in flight
+    if (k == 0) {
+      if (NS == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (NS == 3) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave's pieces landed
+    const int slot = k % NS, pslot = (k + NS - 1) % NS;
+    const bf16_t* Ks = smem + slot * SLOT;
+    const bf16_t* Vs = Ks + IMG;
+    const int ln = remat(lane), qs = ln & 15, gs = ln >> 4;
+    // row 16t + qs of an image has swizzle (qs & 6) for every t: a lane's two chunk offsets are loop constants and the
+    // 16-row tiles are immediate offsets
+    const int o0 = qs * HD + ((gs ^ (qs & 6)) << 3), o1 = qs * HD + (((4 + gs) ^ (qs & 6)) << 3);
+    const bf16_t* Qs = smem + pslot * SLOT + wave * 16 * HD;
+    const bf16x8_t qf0 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(Qs + o0));
+    const bf16x8_t qf1 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(Qs + o1));
+
+    // S^T[key][q] = sum_d K[key][d] Q[q][d]: A = K rows (16-B reads), B = Q fragments
+    f32x4 s[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bf16x8_t k0 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(Ks + t * 16 * HD + o0));
+      const bf16x8_t k1 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(Ks + t * 16 * HD + o1));
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf0, a, 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf1, a, 0, 0, 0);
+    }
+    // every wave is past its K and Q reads: the next item's Q into this slot's K image, then the ring's next K / V
+    // into the slot the previous item used (its Q image was read above)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    q_item(clampi(it + G), slot);
+    kv_item(clampi(it + (NS - 1) * G), pslot);
+
+    // keys >= T only in the last tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((NT - 1) * 16 + 4 * g + i >= Tn) s[NT - 1][i] = -INFINITY;
+    float mx[4] = {s[0][0], s[0][1], s[0][2], s[0][3]};
+#pragma unroll
+    for (int t = 1; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx[i] = fmaxf(mx[i], s[t][i]);
+    float m = fmaxf(fmaxf(mx[0], mx[1]), fmaxf(mx[2], mx[3]));
+    {
+      const auto a32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+      m = fmaxf(__uint_as_float(a32[0]), __uint_as_float(a32[1]));
+      const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+      m = fmaxf(__uint_as_float(a16[0]), __uint_as_float(a16[1]));
+    }
+    const float mc = m * c2;
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], c2, -mc));   // masked keys: exp2(-inf) = 0
+        s[t][i] = p;
+        ls[i] += p;
+      }
+    float l = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+    {
+      const auto a32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(a32[0]) + __uint_as_float(a32[1]);
+      const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      l = __uint_as_float(a16[0]) + __uint_as_float(a16[1]);
+    }
+    // O^T[d][q] += V^T[d][keys] P^T[keys][q], 32 keys per step: tiles (2j, 2j + 1); an odd NT's last step pairs tile
+    // NT - 1 with zeros (its second V read re-reads tile NT - 1's rows: in bounds, multiplied by 0).  Transposed read:
+    // lane 4q + p of a 16-lane group reads row 16t + 4g + q (swizzle (4g + q) & 6 for every t), columns 16 dt + 4p ..:
+    // chunk 2 dt + (p >> 1) sits at 2 (dt ^ (sw >> 1)) + (p >> 1) -> one lane offset per dt
+    f32x4 oacc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                     f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int tq = (ln >> 2) & 3, tp = ln & 3, vr = 4 * gs + tq, sw = vr & 6;
+    int vo[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) vo[dt] = vr * HD + ((2 * (dt ^ (sw >> 1)) + (tp >> 1)) << 3) + 4 * (tp & 1);
+#pragma unroll
+    for (int j = 0; j < (NT + 1) / 2; ++j) {
+      const int t0 = 2 * j, t1 = 2 * j + 1 < NT ? 2 * j + 1 : 2 * j;
+      float pv[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pv[i] = s[t0][i];
+        pv[4 + i] = 2 * j + 1 < NT ? s[t1][i] : 0.f;
+      }
+      const bf16x8_t pb = pack8(pv);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const s16x4 lo = tr_read(Vs + t0 * 16 * HD + vo[dt]);
+        const s16x4 hi = tr_read(Vs + t1 * 16 * HD + vo[dt]);
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, v), pb, oacc[dt], 0, 0, 0);
+      }
+    }
+    // lane (q, g) holds O[q][16 dt + 4 g + i]
+    const int64_t b = it / H, h = it - (it / H) * H;
+    const float inv = 1.0f / l;
+    const bool qok = q < Tn;
+    bf16_t* orow = o + (b * Tn + q) * D + h * HD + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+      if (qok) st4<bf16_t>(orow + 16 * dt, v);
+    }
+    if (qok && g == 0) lse[(b * H + h) * Tn + q] = (mc + log2f(l)) / LOG2E;
+    if (o32 != nullptr && qok) {                      // the tiled backward's exact delta (attn_bwd_split forced)
+      float* orow32 = o32 + (b * Tn + q) * D + h * HD + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const float v[4] = {oacc[dt][0] * inv, oacc[dt][1] * inv, oacc[dt][2] * inv, oacc[dt][3] * inv};
+        st4<float>(orow32 + 16 * dt, v);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }
 
 }  // namespace
@@ -1286,7 +1487,19 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && probs == nullptr) {
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
-    if (T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_FWD_SPLIT)) {
+    if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING)) {
+      const int64_t items = B * H;
+      const unsigned grid = (unsigned)std::min<int64_t>(items, vit_cu_count());
+#define RING(NT) \
+  attn_fwd_ring<NT><<<grid, NT * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, items, scale)
+      switch ((int)((T + 15) / 16)) {
+        case 1: RING(1); break;   case 2: RING(2); break;   case 3: RING(3); break;   case 4: RING(4); break;
+        case 5: RING(5); break;   case 6: RING(6); break;   case 7: RING(7); break;   case 8: RING(8); break;
+        case 9: RING(9); break;   case 10: RING(10); break; case 11: RING(11); break; case 12: RING(12); break;
+        case 13: RING(13); break; case 14: RING(14); break; case 15: RING(15); break; default: RING(16); break;
+      }
+#undef RING
+    } else if (T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_FWD_SPLIT)) {
 #define FWD(NK) \
   attn_fwd_fused<NK><<<(unsigned)(B * H), NK * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, scale)
       switch ((int)((T + 31) / 32)) {
