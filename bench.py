@@ -254,8 +254,11 @@ def run(args, rank, world, local):
         D = L = T = N = 0
         cfg = None
     else:
-        from VisionTransformer import config, vit
+        from VisionTransformer import _lib, config, vit
         from VisionTransformer.optim import FusedAdamW, cross_entropy
+        for kv in args.opt:
+            name, val = kv.split("=")
+            _lib.set_option(name, int(val))
         cfg = config.ViTConfig.preset(args.model, img_size=args.img, batch_size=args.batch, num_classes=args.classes,
                                       precision=dtype, device="cpu")
         torch.manual_seed(0)                       # identical init on every rank (reference init order, CPU RNG)
@@ -348,6 +351,8 @@ def run(args, rank, world, local):
                        "model": f"vit_{args.model}_patch16_{args.img}", "global_batch": args.batch * world,
                        "seq_len": T, "parallelism": f"dp{world}"},
         }
+        if args.opt:
+            out["options"] = dict(kv.split("=") for kv in args.opt)
         if world > 1:
             out["comm_exposed_ms"] = round(comm, 3) if comm is not None else None
             out["grad_comm_dtype"] = args.grad_comm
@@ -459,6 +464,8 @@ def main(argv=None):
     ap.add_argument("--roctx", action="store_true",
                     help="roctx ranges per kernel family (rocprofv3 --marker-trace timelines; costs host time)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo stand-in step: tests rank launch without a GPU")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library launch option (vit_set_option; A/B runs of kernel variants, default: shipped)")
     args = ap.parse_args(argv)
 
     if "WORLD_SIZE" in os.environ:           # launched by torchrun: one rank per process

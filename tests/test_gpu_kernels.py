@@ -466,17 +466,18 @@ def _attn_ref(qkv, B, T, H, hd, scale):
     return o, lse, p
 
 
-@pytest.mark.parametrize("shape", ["proj_fwd", "fc2_fwd", "dgrad_qkv", "fc1_fwd", "dgrad_fc2m"])
+@pytest.mark.parametrize("shape", ["proj_fwd", "fc2_fwd", "dgrad_qkv", "fc1_fwd", "dgrad_fc2m", "dgrad_proj"])
 def test_gemm_c2_shapes_tail_split(libopt, shape):
     """The forward / input-gradient GEMMs at their real C2 shapes (M = 50,432: 591 / 2,364 tiles over 256 CUs, the
-    persistent grid).  With the split-K tail (option gemm_tail, on: N = 768 and K >= 2048 run the last partial round
-    split over K with fp32 slabs) against whole tiles only (gemm_tail 0): the same outputs to bf16 rounding of a
-    different fp32 summation order, identical keep / ReLU bits where the pre-rounding values agree, bitwise run to
-    run, and within bf16 tolerance of an fp32 torch product."""
+    persistent grid).  With the tails of a last partial round — the split-K tail (option gemm_tail: N = 768 and
+    K >= 2048 run it split over K with fp32 slabs) and the 128x128-tile tail (option gemm_tail_v2: the K = 768 shapes
+    run its tile rows as quarter tiles, two workgroups per CU; round 5) — against whole 256x256 tiles only: the same
+    outputs to bf16 rounding of a different fp32 summation order, identical keep / ReLU bits where the pre-rounding
+    values agree, bitwise run to run, and within bf16 tolerance of an fp32 torch product."""
     M, D = 256 * 197, 768
     m, n, k, bkc, kind = {"proj_fwd": (M, D, D, True, "bdr"), "fc2_fwd": (M, D, 4 * D, True, "bdr"),
                           "dgrad_qkv": (M, D, 3 * D, False, "plain"), "fc1_fwd": (M, 4 * D, D, True, "relu_mask"),
-                          "dgrad_fc2m": (M, 4 * D, D, False, "auxm")}[shape]
+                          "dgrad_fc2m": (M, 4 * D, D, False, "auxm"), "dgrad_proj": (M, D, D, False, "plain")}[shape]
     g = torch.Generator(device=DEV).manual_seed(11)
     a = (torch.rand(m, k, device=DEV, generator=g) * 2 - 1).bfloat16()
     b = (torch.rand(n, k, device=DEV, generator=g) * 2 - 1).bfloat16() if bkc else \
@@ -499,6 +500,7 @@ def test_gemm_c2_shapes_tail_split(libopt, shape):
     c1b, m1b = run()
     assert torch.equal(c1, c1b) and torch.equal(m1, m1b)                 # deterministic
     libopt("gemm_tail", 0)
+    libopt("gemm_tail_v2", 0)
     c0, m0 = run()
     ref = a.float() @ (b.float().t() if bkc else b.float())
     scale = float(ref.abs().max())

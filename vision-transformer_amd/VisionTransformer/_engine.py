@@ -118,6 +118,7 @@ class Engine:
         self._comm_events = None
         self._works = []
         self._ws = None
+        self._tok = None
         self._ptr_sig = None
         self._ver_sig = None
         self.stats = {"packs": 0}
@@ -291,6 +292,18 @@ class Engine:
         self._ver_sig = self._version_signature()
 
     # ------------------------------------------------------------------------------------------------------------
+    def _token_rows(self, name, M, D, dt, T, dev):
+        """[M, D] buffer that is zero outside the token-0 rows b*T (the pruned last block's attention-backward operands):
+        allocated zeroed once per shape; every use writes exactly rows b*T again, so the rest stays zero and no
+        M x D fill runs per step."""
+        key = (name, M, D, dt, T, dev)
+        buf = self._tok.get(key) if self._tok is not None else None
+        if buf is None:
+            if self._tok is None:
+                self._tok = {}
+            buf = self._tok[key] = torch.zeros(M, D, dtype=dt, device=dev)
+        return buf
+
     def _workspace(self, nbytes):
         if self._ws is None or self._ws.numel() * 4 < nbytes:
             self._ws = torch.empty(max(nbytes // 4 + 1, 1 << 20), dtype=torch.float32, device=self.device)
@@ -738,9 +751,9 @@ class Engine:
         mk("gemm_dgrad", 1)
         if pr:
             # back to all M rows for the attention backward (zero outside the token-0 rows)
-            do_full = torch.zeros(M, D, dtype=dt, device=dev)
+            do_full = self._token_rows("do", M, D, dt, T, dev)
             _ops.copy2d(do, D, do_full, T * D, B, D)
-            dxm_full = torch.zeros(M, D, dtype=dt, device=dev)
+            dxm_full = self._token_rows("dxm", M, D, dt, T, dev)
             _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
             do, dx_mid = do_full, dxm_full
         if o32 is None and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):

@@ -626,7 +626,8 @@ constexpr int FB_TMAX = 256;
 #ifndef ATT_KVLDS
 #define ATT_KVLDS 1
 #endif
-#ifndef ATT_ORDER                // A/B builds only: loop-body order (0 back, front, dq; 1 front, back, dq; 2 dq first)
+#ifndef ATT_ORDER                // A/B builds only: loop-body order (0 back, front, dq; 1 front, back, dq; 2 dq first;
+                                 // 3 waves 4-7 dq first)
 #define ATT_ORDER 0
 #endif
 #ifndef ATT_PRIO                 // A/B builds only: s_setprio 1 around the S / dP MFMA chain
@@ -1088,6 +1089,19 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
         dq(it - 2);
         back(it - 1);
         front(it);
+#elif ATT_ORDER == 3
+        // SIMD partners (waves w, w + 4) in different phases: waves 4-7 run the LDS / MFMA-heavy dQ tile first while
+        // waves 0-3 run the VALU-heavy delta / dS of back(); back stays before front (front overwrites P / dP)
+        dq_store(it - 3);
+        if (wave < 4) {
+          back(it - 1);
+          front(it);
+          dq(it - 2);
+        } else {
+          dq(it - 2);
+          back(it - 1);
+          front(it);
+        }
 #else
         dq_store(it - 3);
         back(it - 1);
@@ -1318,8 +1332,12 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
   constexpr int Tp = NT * 16;
   constexpr int IMG = Tp * HD;                        // elements of one [Tp][64] image
   constexpr int SLOT = 2 * IMG;                       // K then V
-  constexpr int NS = 3 * SLOT * 2 <= 160 * 1024 ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * SLOT];
+#ifndef RING_QBUF              // A/B builds: 1 = two K/V slots + a Q double buffer, one barrier per item
+#define RING_QBUF 0
+#endif
+  constexpr bool QB = RING_QBUF && 6 * IMG * 2 <= 160 * 1024;
+  constexpr int NS = !QB && 3 * SLOT * 2 <= 160 * 1024 ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * SLOT + (QB ? 2 * IMG : 0)];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, ql = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Tn = (int)Tn64;
@@ -1336,10 +1354,11 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
       ring_piece(qkv, b * Tn, ld, 2 * D + h * HD, Tn, Ks + IMG, 2 * wave + i, lane);
     }
   };
-  auto q_item = [&](int64_t it, int slot) {           // Q pieces 2w, 2w + 1 into the K image of `slot`
+  auto q_item = [&](int64_t it, int slot) {           // Q pieces 2w, 2w + 1 into the K image of `slot` (QB: Q buffer)
     const int64_t b = it / H, h = it - (it / H) * H;
+    bf16_t* dst = QB ? smem + NS * SLOT + slot * IMG : smem + slot * SLOT;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) ring_piece(qkv, b * Tn, ld, h * HD, Tn, smem + slot * SLOT, 2 * wave + i, lane);
+    for (int i = 0; i < 2; ++i) ring_piece(qkv, b * Tn, ld, h * HD, Tn, dst, 2 * wave + i, lane);
   };
 
   int64_t it = blockIdx.x;
@@ -1351,7 +1370,7 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
   const auto clampi = [&](int64_t x) { return x < items ? x : items - 1; };
   // prologue: K/V of the first item (slot 0), its Q (the K image of slot NS - 1), K/V of the second (NS = 3: slot 1)
   kv_item(it, 0);
-  q_item(it, NS - 1);
+  q_item(it, QB ? 0 : NS - 1);
   if (NS == 3) kv_item(clampi(it + G), 1);
 #pragma unroll 1
   for (int k = 0; it < items; it += G, ++k) {
@@ -1369,11 +1388,15 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
     const int slot = k % NS, pslot = (k + NS - 1) % NS;
     const bf16_t* Ks = smem + slot * SLOT;
     const bf16_t* Vs = Ks + IMG;
+    if (QB) {                                         // the next item's Q and K / V: the buffers item k - 1 used
+      q_item(clampi(it + G), (k + 1) & 1);
+      kv_item(clampi(it + G), pslot);
+    }
     const int ln = remat(lane), qs = ln & 15, gs = ln >> 4;
     // row 16t + qs of an image has swizzle (qs & 6) for every t: a lane's two chunk offsets are loop constants and the
     // 16-row tiles are immediate offsets
     const int o0 = qs * HD + ((gs ^ (qs & 6)) << 3), o1 = qs * HD + (((4 + gs) ^ (qs & 6)) << 3);
-    const bf16_t* Qs = smem + pslot * SLOT + wave * 16 * HD;
+    const bf16_t* Qs = (QB ? smem + NS * SLOT + (k & 1) * IMG : smem + pslot * SLOT) + wave * 16 * HD;
     const bf16x8_t qf0 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(Qs + o0));
     const bf16x8_t qf1 = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(Qs + o1));
 
@@ -1389,9 +1412,11 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
     }
     // every wave is past its K and Q reads: the next item's Q into this slot's K image, then the ring's next K / V
     // into the slot the previous item used (its Q image was read above)
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    q_item(clampi(it + G), slot);
-    kv_item(clampi(it + (NS - 1) * G), pslot);
+    if (!QB) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      q_item(clampi(it + G), slot);
+      kv_item(clampi(it + (NS - 1) * G), pslot);
+    }
 
     // keys >= T only in the last tile
 #pragma unroll

@@ -1523,6 +1523,28 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
   return (int)sk;
 }
 
+// Option gemm_tail_v2 (off by default): the rows of a last partial round of 256x256 tiles that the split-K tail does
+// not take (K below gemm_tail_min_kt k-tiles: proj and its input gradient, fc1, the fc2 input gradient at ViT-B/16
+// C2) run as 128x128 tiles (v2, two workgroups per CU): the 81 tiles of the third round of an N = 768 GEMM become 324
+// quarter-tiles that all run at once, instead of 81 whole tiles on a third of the CUs.  Measured (round 5, one box,
+// bench.py --opt gemm_tail_v2=0/1): 31.6 vs 33.0 ms/step — the v2 tiles with the general epilogue (and the separate
+// column-sum pass) cost more than the idle CUs of the whole-tile round.  Returns 1 and *m_main = the rows of the
+// whole rounds.
+int tail_rows_v2(const vit_gemm_desc* d, int64_t* m_main) {
+  *m_main = d->m;
+  if (!vit::opt(vit::OPT_GEMM_TAIL_V2)) return 0;
+  if (d->split_k > 1 || d->in_dtype != VIT_BF16 || d->k % BK != 0 || d->m <= 0 || d->n <= 0) return 0;
+  if (gemm_impl(d->m, d->n) != 4 || d->out_group_rows != 0 || d->res_rowmod != 0) return 0;
+  const int64_t tn = (d->n + 255) / 256, tm = (d->m + 255) / 256;
+  const int64_t rounds = tm * tn / 256;
+  if (rounds < 1) return 0;
+  const int64_t mr = rounds * 256 / tn;                    // tile rows that fill whole rounds
+  const int64_t tail = (tm - mr) * tn;
+  if (tail <= 0 || 2 * tail > 256) return 0;
+  *m_main = mr * 256;
+  return 1;
+}
+
 }  // namespace
 
 
@@ -1555,7 +1577,7 @@ extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dty
 
 // One GEMM launch (+ the split-K reduce, + the column-sum pass when it is not fused); row0 = global row of local
 // row 0 (dropout indices).
-static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
+static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream, int force_impl = 0) {
   VIT_REQUIRE(d != nullptr, "vit_gemm: null descriptor");
   VIT_REQUIRE(d->a && d->b && d->c, "vit_gemm: null operand pointer");
   VIT_REQUIRE(!d->colsum_part || d->out_group_rows == 0, "vit_gemm: colsum_part needs ungrouped output rows");
@@ -1627,7 +1649,7 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
     const int64_t a_bytes = (akc ? (d->m - 1) * d->lda + d->k : (d->k - 1) * d->lda + d->m) * 2;
     const int64_t b_bytes = (bkc ? (d->n - 1) * d->ldb + d->k : (d->k - 1) * d->ldb + d->n) * 2;
     // v2/v4 (LDS-DMA) need whole 64-deep k-tiles (split boundaries are k-tile aligned) and operands < 2 GiB
-    const int impl = gemm_impl(d->m, d->n);
+    const int impl = force_impl ? force_impl : gemm_impl(d->m, d->n);
     const bool dma_ok = d->k % BK == 0 && a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL;
     const bool v2 = impl == 2 && dma_ok;
     const bool v4 = (impl == 4 || impl == 3) && dma_ok;
@@ -1742,8 +1764,10 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream) {
 extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
   VIT_REQUIRE(d != nullptr, "vit_gemm: null descriptor");
   int64_t m_main = 0;
-  const int sk = tail_split(d, &m_main);
-  if (sk > 1 && d->workspace && d->workspace_bytes >= vit_gemm_workspace_bytes(d)) {
+  int sk = tail_split(d, &m_main);
+  const bool split_tail = sk > 1 && d->workspace && d->workspace_bytes >= vit_gemm_workspace_bytes(d);
+  const bool v2_tail = !split_tail && tail_rows_v2(d, &m_main);
+  if (split_tail || v2_tail) {
     vit_gemm_desc dm = *d;
     dm.m = m_main;
     const int rc = gemm_run(&dm, 0, stream);
@@ -1759,6 +1783,7 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     if (d->res) dt.res = (const char*)d->res + r * d->ldres * esz(d->res_dtype);
     if (d->colsum_part) dt.colsum_part = d->colsum_part + (r / 256) * d->n;
     dt.m = d->m - r;
+    if (v2_tail) return gemm_run(&dt, r, stream, 2);
     dt.split_k = sk;
     return gemm_run(&dt, r, stream);
   }
