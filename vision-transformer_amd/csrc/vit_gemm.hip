@@ -679,6 +679,9 @@ VIT_DEV void dma_half_g(const char* base, const uint32_t (&off)[2], uint32_t sof
 #define V4_LEAD (V4_SLOTS - 2)
 #endif
 static_assert(V4_LEAD <= V4_SLOTS - 2 && V4_LEAD >= 4 && V4_LEAD <= 8, "v4 ring: 4 <= LEAD <= SLOTS - 2, LEAD <= 8");
+#ifndef V4_DMA_MFMA      // A/B builds: 1 = a phase's LDS-DMA stage issued between its two MFMA half-clusters
+#define V4_DMA_MFMA 0
+#endif
 
 // vmcnt for phase f: the `left` DMA stages younger than s = f+2 that exist may stay in flight (2 instructions each)
 VIT_DEV void wait_stage_retired(int left) {
@@ -705,6 +708,16 @@ VIT_DEV void read_b4(const bf16_t* half, int wc, int lane, bf16x8_t (&bf)[2][2])
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int y = 0; y < 2; ++y) bf[y][kk] = read_frag<BKC>(half, wc * 32 + y * 16, kk, lane);
+}
+
+// Half of a quadrant's MFMAs (k-step kk of the 64-deep k-tile); V4_DMA_MFMA issues the phase's LDS-DMA between the
+// two halves (the MFMA segment), not in the load segment.
+VIT_DEV void mfma_quadrant_half(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const bf16x8_t (&bf)[2][2], int kk) {
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+      acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[y][kk], af[x][kk], acc[x][y], 0, 0, 0);
 }
 
 VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const bf16x8_t (&bf)[2][2]) {
@@ -1279,6 +1292,31 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 
     // One phase f = 4t + r.  STEADY: the k-tiles before the last two, where every phase issues its DMA stage and the
     // retiring wait is the constant vmcnt(2 * (LEAD - 2)) — no per-phase branches (the tail's counts are computed).
+#if V4_DMA_MFMA
+    // the stage goes out in the MFMA segment (below), after this wait: one stage fewer is in flight here
+#define V4_PHASE_DMA(F, STEADY)                                                                  \
+  do {                                                                                           \
+    if (STEADY) wait_stage_retired(V4_LEAD - 3);                                                 \
+    else wait_stage_retired(min(V4_LEAD - 3, nstage - 1 - ((F) + 2)));                           \
+  } while (0)
+#define V4_MFMA_DMA(ACC, BF, F, STEADY)                                                          \
+  do {                                                                                           \
+    __builtin_amdgcn_s_setprio(1);                                                               \
+    mfma_quadrant_half(ACC, af, BF, 0);                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if (STEADY || (F) + V4_LEAD < nstage) V4_STAGE((F) + V4_LEAD);                               \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    mfma_quadrant_half(ACC, af, BF, 1);                                                          \
+    __builtin_amdgcn_s_setprio(0);                                                               \
+  } while (0)
+#define V4_PHASE_MFMA(R, F, STEADY)                                                              \
+  do {                                                                                           \
+    if ((R) == 0) V4_MFMA_DMA(acc[0][0], b0f, F, STEADY);                                        \
+    else if ((R) == 1) V4_MFMA_DMA(acc[0][1], b1f, F, STEADY);                                   \
+    else if ((R) == 2) V4_MFMA_DMA(acc[1][1], b1f, F, STEADY);                                   \
+    else V4_MFMA_DMA(acc[1][0], b0f, F, STEADY);                                                 \
+  } while (0)
+#else
 #define V4_PHASE_DMA(F, STEADY)                                                                  \
   do {                                                                                           \
     if (STEADY) {                                                                                \
@@ -1289,13 +1327,14 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
       wait_stage_retired(min(V4_LEAD - 2, nstage - 1 - ((F) + 2)));                              \
     }                                                                                            \
   } while (0)
-#define V4_PHASE_MFMA(R)                                                                         \
+#define V4_PHASE_MFMA(R, F, STEADY)                                                              \
   do {                                                                                           \
     if ((R) == 0) mfma_quadrant(acc[0][0], af, b0f);                                             \
     else if ((R) == 1) mfma_quadrant(acc[0][1], af, b1f);                                        \
     else if ((R) == 2) mfma_quadrant(acc[1][1], af, b1f);                                        \
     else mfma_quadrant(acc[1][0], af, b0f);                                                      \
   } while (0)
+#endif
 #define V4_PHASE(T, R, STEADY)                                                                   \
   do {                                                                                           \
     const int f_ = 4 * (T) + (R);                                                                \
@@ -1311,7 +1350,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
     __builtin_amdgcn_sched_barrier(0);                                                           \
     __builtin_amdgcn_s_barrier();                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                           \
-    V4_PHASE_MFMA(R);                                                                            \
+    V4_PHASE_MFMA(R, f_, STEADY);                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                           \
     __builtin_amdgcn_s_barrier();                                                                \
     __builtin_amdgcn_sched_barrier(0);                                                           \
@@ -1333,6 +1372,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 #undef V4_PHASE
 #undef V4_PHASE_MFMA
 #undef V4_PHASE_DMA
+#ifdef V4_MFMA_DMA
+#undef V4_MFMA_DMA
+#endif
     if (wr == 0) __builtin_amdgcn_s_barrier();            // balance group 1's extra barrier
 
     // next item: its first stages go out now (slots 0-3), ahead of this tile's epilogue
