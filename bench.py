@@ -54,12 +54,17 @@ def gflop_per_image(D, L, T, N, P, C, nc):
     return (2 * pe + 3 * (L * block + head)) / 1e9
 
 
-def gflop_executed_per_image(D, L, T, N, P, C, nc, pruned):
-    """GFLOP per image the kernels actually execute: the reference count minus the last block's proj / fc1 / fc2
-    (fwd, dgrad, wgrad: 54 D^2 per token) on the T-1 rows the pruned last block skips (its outputs and
-    gradients are identical to the unpruned engine's, tested)."""
+def gflop_executed_per_image(D, L, T, N, P, C, nc, pruned, row0=True):
+    """GFLOP per image the kernels actually execute: the reference count minus what the pruned last block skips
+    (its outputs and gradients are identical to the unpruned engine's, tested): proj / fc1 / fc2 (fwd,
+    dgrad, wgrad: 54 D^2 per token) on the T-1 rows other than token 0, and its attention on queries other than 0
+    (12 T^2 D fwd + bwd -> 14 T D for query 0 alone) with the Q third of its QKV GEMMs (fwd, dgrad, wgrad: 6 D^2 per
+    token) on rows other than token 0 (round 5)."""
     full = gflop_per_image(D, L, T, N, P, C, nc)
-    return full - (54.0 * D * D * (T - 1) / 1e9 if pruned else 0.0)
+    if not pruned:
+        return full
+    att = 12.0 * T * T * D - 14.0 * T * D + 6.0 * D * D * (T - 1) if row0 else 0.0
+    return full - (54.0 * D * D * (T - 1) + att) / 1e9
 
 
 def workload_key(args):
@@ -263,6 +268,12 @@ def run(args, rank, world, local):
                                       precision=dtype, device="cpu")
         torch.manual_seed(0)                       # identical init on every rank (reference init order, CPU RNG)
         model = vit.VisionTransformer(cfg).to(dev).train()
+        for kv in args.engine:
+            name, val = kv.split("=")
+            if not hasattr(model.hip_engine, name):
+                raise SystemExit(f"--engine: no Engine attribute {name!r}")
+            setattr(model.hip_engine, name, bool(int(val)) if isinstance(getattr(model.hip_engine, name), bool)
+                    else int(val))
         if world > 1:
             model.enable_data_parallel(grad_dtype=torch.bfloat16 if args.grad_comm == "bf16" else torch.float32,
                                        launch_mode=args.launch_mode)
@@ -353,6 +364,8 @@ def run(args, rank, world, local):
         }
         if args.opt:
             out["options"] = dict(kv.split("=") for kv in args.opt)
+        if args.engine:
+            out["engine"] = dict(kv.split("=") for kv in args.engine)
         if world > 1:
             out["comm_exposed_ms"] = round(comm, 3) if comm is not None else None
             out["grad_comm_dtype"] = args.grad_comm
@@ -365,7 +378,9 @@ def run(args, rank, world, local):
             peak = PEAK_BF16 if dtype == torch.bfloat16 else PEAK_F32
             out["step_mfma_frac"] = round(imgs * gf * 1e9 / (world * peak), 4)
             out["gflop_per_image"] = round(gf, 3)
-            gfx = gflop_executed_per_image(D, L, T, N, cfg.patch_size, 3, args.classes, model.hip_engine.prune_last)
+            eng = model.hip_engine
+            gfx = gflop_executed_per_image(D, L, T, N, cfg.patch_size, 3, args.classes, eng.prune_last,
+                                           eng.row0_attention)
             out["step_mfma_frac_executed"] = round(imgs * gfx * 1e9 / (world * peak), 4)
             out["gflop_executed_per_image"] = round(gfx, 3)
             out["final_loss"] = round(final_loss, 4)
@@ -464,6 +479,8 @@ def main(argv=None):
     ap.add_argument("--roctx", action="store_true",
                     help="roctx ranges per kernel family (rocprofv3 --marker-trace timelines; costs host time)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo stand-in step: tests rank launch without a GPU")
+    ap.add_argument("--engine", action="append", default=[], metavar="ATTR=INT",
+                    help="set an Engine attribute for A/B runs (e.g. row0_attention=0, prune_last=0)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library launch option (vit_set_option; A/B runs of kernel variants, default: shipped)")
     args = ap.parse_args(argv)

@@ -11,7 +11,7 @@ from oracle import vit_oracle as O
 pytestmark = pytest.mark.gpu
 
 if torch.cuda.is_available():
-    from VisionTransformer import _ops  # noqa: E402
+    from VisionTransformer import _lib, _ops  # noqa: E402
 
 DEV = "cuda"
 
@@ -548,6 +548,62 @@ def test_attention_fwd_bwd(dtype, hd, T, amp):
     _check_attn_bwd_bf16(dqkv, _attn_flash_grads(qkv, d_o, B, T, H, hd, scale), D)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("T,hd", [(1, 64), (5, 64), (197, 64), (197, 32), (577, 64), (2500, 16)])
+def test_attention_row0_fwd_bwd(dtype, T, hd):
+    """Query 0 only (vit_attn_fwd_row0 / vit_attn_bwd_row0, the pruned last block): o row 0 and lse[.., 0] equal the
+    full attention's row 0; with an output gradient on row 0 only, dQ row 0 and all of dK / dV equal the full
+    backward's, and the dQ rows 1..T-1 (and o rows 1..T-1) are left untouched.  fp32 to 2e-5 of the scale (fp64
+    reference), bf16 to 1e-2 of the norm (the kernels compute in fp32 and round once)."""
+    torch.manual_seed(T + hd)
+    B, H = 3, 2
+    D = H * hd
+    scale = hd ** 0.5
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).to(dtype)
+    o = torch.full((B * T, D), 7.0, device=DEV, dtype=dtype)
+    o, lse = _ops.attn_fwd_row0(qkv, B, T, H, hd, scale, o=o)
+    x = qkv.double().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    p = torch.softmax(s, -1)
+    o_ref = (p @ v).permute(0, 2, 1, 3).reshape(B * T, D)
+    rows = torch.arange(B, device=DEV) * T
+    others = torch.ones(B * T, dtype=torch.bool, device=DEV)
+    others[rows] = False
+    assert bool((o[others] == 7.0).all())                               # untouched
+    got, ref = o[rows].double(), o_ref[rows].detach()
+    if dtype == torch.float32:
+        assert float((got - ref).abs().max()) <= 2e-5 * max(1.0, float(ref.abs().max()))
+    else:
+        assert float((got - ref).norm() / ref.norm()) < 1e-2
+    lse_ref = torch.logsumexp(s, -1)[:, :, 0]
+    assert float((lse[:, :, 0].double() - lse_ref).abs().max()) <= 1e-4 * max(1.0, float(lse_ref.abs().max()))
+    g0 = torch.randn(B, D, device=DEV).to(dtype)
+    d_o = torch.zeros(B * T, D, device=DEV, dtype=torch.float64)
+    d_o[rows] = g0.double()
+    o_ref.backward(d_o)
+    dqkv = torch.full((B * T, 3 * D), 5.0, device=DEV, dtype=dtype)
+    dqkv[:, D:] = 0
+    _ops.attn_bwd_row0(qkv, g0, D, lse, dqkv, B, T, H, hd, scale)
+    torch.cuda.synchronize()
+    assert bool((dqkv[others, :D] == 5.0).all())                       # dQ rows 1..T-1 untouched
+    gref = x.grad
+    floor = 1e-3 * float(gref.abs().max())       # T = 1: dQ0 is 0 exactly (one key), the kernel's is rounding-sized
+    for name, sel in (("dQ0", (rows, slice(0, D))), ("dK", (slice(None), slice(D, 2 * D))),
+                      ("dV", (slice(None), slice(2 * D, 3 * D)))):
+        a, r = dqkv[sel].double(), gref[sel]
+        if dtype == torch.float32:
+            err = float((a - r).abs().max()) / max(floor, float(r.abs().max()))
+            assert err <= 2e-5, (name, err)
+        else:
+            err = float((a - r).norm() / max(float(r.norm()), floor * r.numel() ** 0.5))
+            assert err < 1e-2, (name, err)
+    again = torch.full_like(dqkv, 5.0)
+    again[:, D:] = 0
+    _ops.attn_bwd_row0(qkv, g0, D, lse, again, B, T, H, hd, scale)
+    assert torch.equal(again, dqkv)                                     # deterministic
+
+
 @pytest.mark.parametrize("B,H,T", [(1, 1, 1), (3, 3, 33), (3, 3, 65), (1, 5, 129), (3, 1, 300), (2, 3, 577)])
 def test_attention_tiled_kernels_any_grid(libopt, B, H, T):
     """The tiled T > 256 kernels forced at any T (attn_fwd_split / attn_bwd_split): the XCD-aware (block, head) remap
@@ -701,6 +757,34 @@ def test_misc_kernels():
     _ops.dropout_bwd(t, y, 0.2, 4242)
     keep = dropout_keep(4242, (3000,)).to(DEV)
     assert torch.equal(y, t * keep * 1.25)
+
+
+def test_adamw_vector_path_bitwise_equals_scalar():
+    """adamw_vec (16-B accesses on aligned chunks) == one element per lane, bit for bit: aligned and misaligned
+    (offset-1 views) tensors, lengths not a multiple of 4, chunks split at 64 Ki, fp32 and bf16 shadows."""
+    torch.manual_seed(8)
+    base = torch.randn(200003, device=DEV)
+    views = [base[:70001], base[70001 + 3:70001 + 3 + 301], base[1:130001 + 1], base[4:4 + 4096]]
+    outs = []
+    for vec in (1, 0):
+        for sdt in (torch.bfloat16, torch.float32):
+            ps = [v.clone() if i != 2 else torch.cat([torch.zeros(1, device=DEV), v])[1:] for i, v in enumerate(views)]
+            gs = [torch.randn_like(p) for p in ps]
+            ms = [torch.randn_like(p) * 0.1 for p in ps]
+            vs = [torch.rand_like(p) * 0.1 for p in ps]
+            sh = [torch.empty(p.shape, dtype=sdt, device=DEV) for p in ps]
+            table, n = _ops.build_chunk_table(list(zip(ps, gs, ms, vs, sh)), DEV)
+            old = _lib.get_option("adamw_vec")
+            _lib.set_option("adamw_vec", vec)
+            try:
+                for step in range(1, 3):
+                    _ops.adamw(table, n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1 - 0.9 ** step, 1 - 0.999 ** step, 0.5, sdt)
+                torch.cuda.synchronize()
+            finally:
+                _lib.set_option("adamw_vec", old)
+            outs.append([t.clone() for t in ps + ms + vs + sh])
+    for a, b in zip(outs[:2], outs[2:]):
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
 def test_adamw_matches_torch():

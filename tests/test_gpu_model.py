@@ -264,7 +264,8 @@ def test_vit_base_224_bf16_full_size_properties():
 
 @pytest.mark.parametrize("dtype,train", [(torch.float32, True), (torch.float32, False), (torch.bfloat16, True)])
 def test_pruned_last_block_matches_all_rows(dtype, train):
-    """The last block's proj / LN2 / MLP on the B token-0 rows only (engine.prune_last, default) == all B*T rows
+    """The last block's proj / LN2 / MLP on the B token-0 rows only (engine.prune_last, default), with its attention
+    on query 0 alone (engine.row0_attention, default) or through the full attention kernels, == all B*T rows
     (prune_last = False): the classifier reads token 0 only (vit.py:80).  Same dropout bits (drawn at the full
     tensor's indices).  ViT-B width, 2 blocks; fp32 to summation-order rounding, bf16 to a few storage roundings."""
     ocfg = O.make_config("micro", img=64, batch=8, blocks=2)
@@ -272,9 +273,10 @@ def test_pruned_last_block_matches_all_rows(dtype, train):
     st = O.init_state(ocfg, seed=5)
     x, y = O.synthetic_batch(ocfg)
     out = []
-    for prune in (True, False):
+    for prune, row0 in ((True, True), (True, False), (False, True)):       # row0: query-0 attention kernels
         m = _model(ocfg, dtype=dtype)
         m.hip_engine.prune_last = prune
+        m.hip_engine.row0_attention = row0
         m.load_state_dict(st)
         m.train(train)
         torch.manual_seed(11)
@@ -283,10 +285,11 @@ def test_pruned_last_block_matches_all_rows(dtype, train):
         loss.backward()
         out.append((logits.detach().cpu(), loss.item(), _grads(m)))
     tol = 1e-4 if dtype == torch.float32 else 2e-2       # Q/K weight gradients amplify summation-order rounding
-    assert _rel(out[0][0], out[1][0]) < tol
-    assert abs(out[0][1] - out[1][1]) < tol * max(1.0, abs(out[1][1]))
-    for k in out[1][2]:
-        assert _rel(out[0][2][k], out[1][2][k]) < tol, (k, _rel(out[0][2][k], out[1][2][k]))
+    for a in out[:2]:
+        assert _rel(a[0], out[2][0]) < tol
+        assert abs(a[1] - out[2][1]) < tol * max(1.0, abs(out[2][1]))
+        for k in out[2][2]:
+            assert _rel(a[2][k], out[2][2][k]) < tol, (k, _rel(a[2][k], out[2][2][k]))
 
 
 def test_side_stream_weight_gradients_bitwise_equal():

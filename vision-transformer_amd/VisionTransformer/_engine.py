@@ -138,6 +138,10 @@ class Engine:
         self._wws = None
         # the last block's post-attention part on the B token-0 rows only (see forward); False: every row (tests)
         self.prune_last = True
+        # ... and its attention on query 0 alone (vit_attn_fwd_row0 / vit_attn_bwd_row0); False: the full attention
+        # kernels with the output gradient zero outside row 0 (A/B runs; set it between steps, not between a forward
+        # and its backward)
+        self.row0_attention = True
 
     # ------------------------------------------------------------------------------------------------------------
     # layout
@@ -482,20 +486,42 @@ class Engine:
         mk("ln_fwd", 0, 0.0, ln_b)
         a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
         mk("ln_fwd", 1)
-        mk("gemm_fwd", 0, 2.0 * M * 3 * D * D, (M * D + 3 * D * D + 3 * M * D) * es)
-        qkv = _ops.linear(a1, self.ww[f"{l}.qkv_w"])                                # 3H heads' K/Q/V in one GEMM
-        mk("gemm_fwd", 1)
+        r0 = pr and self.row0_attention and not want_probs      # the pruned block's attention on query 0 alone
+        wq = self.ww[f"{l}.qkv_w"]
+        if r0:
+            # ... which reads Q of the token-0 rows only: K / V of every row (one GEMM into columns D..3D), Q of the
+            # B token-0 rows (split-K over the idle CUs); the other Q rows of qkv are never read
+            qkv = torch.empty(M, 3 * D, dtype=dt, device=dev)
+            mk("gemm_fwd", 0, 2.0 * M * 2 * D * D, (M * D + 2 * D * D + 2 * M * D) * es)
+            _ops.gemm(a1, wq[D:], qkv[:, D:], M, 2 * D, D, D, D, 3 * D)
+            mk("gemm_fwd", 1)
+            mk("gemm_fwd", 0, 2.0 * B * D * D, (2 * B * D + D * D) * es)
+            self._gemm_rows(True, a1, wq, qkv, B, D, D, T * D, D, T * 3 * D)
+            mk("gemm_fwd", 1)
+        else:
+            mk("gemm_fwd", 0, 2.0 * M * 3 * D * D, (M * D + 3 * D * D + 3 * M * D) * es)
+            qkv = _ops.linear(a1, wq)                                               # 3H heads' K/Q/V in one GEMM
+            mk("gemm_fwd", 1)
         probs = None
         if want_probs:
             probs = torch.empty(B, H, T, T, dtype=torch.float32, device=dev)
-        # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta; the
-        # fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
-        o32 = (torch.empty(M, D, dtype=torch.float32, device=dev)
-               if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
-        mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
-                                                                                     else 0))
-        o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
-        mk("attn_fwd", 1)
+        if r0:
+            # the pruned last block: only attention output row 0 of every image is read (the classifier reads token 0,
+            # everything after the attention is per token), and every softmax row is independent -> query 0 alone,
+            # O(T hd) per (image, head); o rows b*T and lse[:, :, 0] are written
+            o32 = None
+            mk("attn_fwd", 0, 4.0 * B * H * T * hd, 2 * M * D * es + 2 * B * D * es + 4 * B * H)
+            o, lse = _ops.attn_fwd_row0(qkv, B, T, H, hd, self.scale)
+            mk("attn_fwd", 1)
+        else:
+            # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta;
+            # the fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
+            o32 = (torch.empty(M, D, dtype=torch.float32, device=dev)
+                   if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
+            mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
+                                                                                         else 0))
+            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
+            mk("attn_fwd", 1)
         blk.multi_head.attention_probs = probs
         blk.multi_head._probs_skipped = probs is None       # a later read warns once (transformer.py)
         # rows of the post-attention part: all M, or (last block, pruned) the B token-0 rows b*T
@@ -750,30 +776,59 @@ class Engine:
                         shared_cus=self.shared_cus)
         mk("gemm_dgrad", 1)
         if pr:
-            # back to all M rows for the attention backward (zero outside the token-0 rows)
-            do_full = self._token_rows("do", M, D, dt, T, dev)
-            _ops.copy2d(do, D, do_full, T * D, B, D)
+            # the ln1 backward's residual gradient on all M rows (zero outside the token-0 rows)
             dxm_full = self._token_rows("dxm", M, D, dt, T, dev)
             _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
-            do, dx_mid = do_full, dxm_full
-        if o32 is None and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
-            # the forward chose the fused backward (no fp32 O kept) and a library option changed since: the tiled
-            # backward would form delta from the bf16 O, inexact under saturated softmax
-            raise RuntimeError("attention backward needs the fp32 O that this forward did not keep: the "
-                               "attn_bwd_split library option changed between forward and backward")
-        # bytes: qkv, dO, dqkv (+ O and o32 for the tiled backward's delta pass)
-        mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 7 * M * D * es + 4 * B * H * T + (M * D * es + 4 * M * D if o32
-                                                                                      is not None else 0))
-        dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
-                             workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32,
-                             shared_cus=self.shared_cus)
-        mk("attn_bwd", 1)
-        if req[f"{l}.qkv_w"]:
-            self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
+            dx_mid = dxm_full
+        if pr and self.row0_attention:
+            # attention backward from the row-0 output gradients alone (the forward computed row 0 only): dQ row 0, all
+            # of dK / dV; the dQ rows 1..T-1 of this buffer are never written, so they stay zero for the dgrad /
+            # wgrad GEMMs below
+            dqkv = self._token_rows("dqkv", M, 3 * D, dt, T, dev)
+            mk("attn_bwd", 0, 10.0 * B * H * T * hd, 4 * M * D * es + 4 * B * D * es + 4 * B * H)
+            _ops.attn_bwd_row0(qkv, do, D, lse, dqkv, B, T, H, hd, self.scale)
+            mk("attn_bwd", 1)
+        else:
+            if pr:
+                # back to all M rows for the full attention backward (zero outside the token-0 rows)
+                do_full = self._token_rows("do", M, D, dt, T, dev)
+                _ops.copy2d(do, D, do_full, T * D, B, D)
+                do = do_full
+            if o32 is None and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
+                # the forward chose the fused backward (no fp32 O kept) and a library option changed since: the tiled
+                # backward would form delta from the bf16 O, inexact under saturated softmax
+                raise RuntimeError("attention backward needs the fp32 O that this forward did not keep: the "
+                                   "attn_bwd_split library option changed between forward and backward")
+            # bytes: qkv, dO, dqkv (+ O and o32 for the tiled backward's delta pass)
+            mk("attn_bwd", 0, 10.0 * B * H * T * T * hd, 7 * M * D * es + 4 * B * H * T + (M * D * es + 4 * M * D if o32
+                                                                                          is not None else 0))
+            dqkv = _ops.attn_bwd(qkv, o, do, lse, B, T, H, hd, self.scale,
+                                 workspace=self._workspace(_ops.attn_bwd_workspace_bytes(B, T, H, hd, dt)), o32=o32,
+                                 shared_cus=self.shared_cus)
+            mk("attn_bwd", 1)
+        wq = self.ww[f"{l}.qkv_w"]
         da1 = torch.empty(M, D, dtype=dt, device=dev)
-        mk("gemm_dgrad", 0, 2.0 * M * 3 * D * D, (3 * M * D + 3 * D * D + M * D) * es)
-        self._gemm_bwd(dqkv, self.ww[f"{l}.qkv_w"], da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
-        mk("gemm_dgrad", 1)
+        if pr and self.row0_attention:
+            # dQ is zero outside the token-0 rows: the K / V part over every row, the Q part over the B token-0 rows
+            # (weight gradient: its own K = B GEMM; input gradient: added onto those rows of da1 by the residual
+            # epilogue, in place)
+            if req[f"{l}.qkv_w"]:
+                gq = gw[f"{l}.qkv_w"]
+                self._wgrad(dqkv[:, D:], a1, gq[D:], 2 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
+                self._wgrad(dqkv, a1, gq[:D], D, D, B, T * 3 * D, T * D, beta, side, "gemm_wgrad")
+            mk("gemm_dgrad", 0, 2.0 * M * 2 * D * D, (2 * M * D + 2 * D * D + M * D) * es)
+            self._gemm_bwd(dqkv[:, D:], wq[D:], da1, M, D, 2 * D, 3 * D, D, D, b_kcontig=False)
+            mk("gemm_dgrad", 1)
+            mk("gemm_dgrad", 0, 2.0 * B * D * D, (3 * B * D + D * D) * es)
+            self._gemm_rows(True, dqkv, wq, da1, B, D, D, T * 3 * D, D, T * D, b_kcontig=False, res=da1,
+                            ldres=T * D, shared_cus=self.shared_cus)
+            mk("gemm_dgrad", 1)
+        else:
+            if req[f"{l}.qkv_w"]:
+                self._wgrad(dqkv, a1, gw[f"{l}.qkv_w"], 3 * D, D, M, 3 * D, D, beta, side, "gemm_wgrad")
+            mk("gemm_dgrad", 0, 2.0 * M * 3 * D * D, (3 * M * D + 3 * D * D + M * D) * es)
+            self._gemm_bwd(dqkv, wq, da1, M, D, 3 * D, 3 * D, D, D, b_kcontig=False)
+            mk("gemm_dgrad", 1)
         dx_in = torch.empty(M, D, dtype=dt, device=dev)
         g1n = torch.empty(M, D, dtype=dt, device=dev) if (training and chain_prev) else None
         # ln1 backward; for l > 0 its third partial set is the column sums of the next g1 (g1n, or dx_in in eval)

@@ -201,6 +201,26 @@ def attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, dqkv=None, workspace=None, o3
     return dqkv
 
 
+def attn_fwd_row0(qkv, B, T, H, hd, scale, o=None, lse=None, stream=None):
+    """Attention output row 0 of every image (vit_attn_fwd_row0): o rows b*T and lse[b][h][0] are written, the other
+    rows / entries are left as they are (o and lse may be fresh, uninitialised tensors)."""
+    _need_cuda(qkv)
+    D = H * hd
+    o = torch.empty(B * T, D, dtype=qkv.dtype, device=qkv.device) if o is None else o
+    lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device) if lse is None else lse
+    _lib.call("vit_attn_fwd_row0", _ptr(qkv), _ptr(o), _ptr(lse), B, T, H, hd, scale, dtype_code(qkv), _stream(stream))
+    return o, lse
+
+
+def attn_bwd_row0(qkv, d_o0, ldo, lse, dqkv, B, T, H, hd, scale, stream=None):
+    """Backward of attn_fwd_row0 from the row-0 output gradients d_o0 (image b at row b, stride ldo): dQ row 0 and all
+    of dK, dV into dqkv (dQ rows 1..T-1 untouched)."""
+    _need_cuda(qkv, d_o0, lse, dqkv)
+    _lib.call("vit_attn_bwd_row0", _ptr(qkv), _ptr(d_o0), ldo, _ptr(lse), _ptr(dqkv), B, T, H, hd, scale,
+              dtype_code(qkv), _stream(stream))
+    return dqkv
+
+
 def colsum(x, rows, cols, ldx, out, beta=0.0, workspace=None, alpha=1.0, stream=None):
     need = _lib.load().vit_colsum_workspace_bytes(rows, cols)
     if workspace is None or workspace.numel() * workspace.element_size() < need:

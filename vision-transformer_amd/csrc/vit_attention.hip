@@ -1502,6 +1502,151 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Query 0 only (vit_attn_fwd_row0 / vit_attn_bwd_row0): one 256-thread workgroup per (image, head); keys on the
+// threads for the scores, the output dimension on the lanes (4 waves over the keys, partials added in wave order)
+// for the value-weighted sums.  Fixed summation orders: deterministic.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int R0_TMAX = 4096, R0_HDMAX = 128;
+
+template <class T>
+VIT_DEV void r0_load_row(const T* p, int hd, float* dst) {          // hd elements -> dst (LDS)
+  for (int d = threadIdx.x; d < hd; d += blockDim.x) dst[d] = ld1<T>(p + d);
+}
+
+// block sum of one float per thread, fixed order (per-wave tree, then waves in order)
+VIT_DEV float r0_block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+VIT_DEV float r0_block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float m = -INFINITY;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+  return m;
+}
+
+// dot of a row (hd elements of T) with an LDS vector
+template <class T>
+VIT_DEV float r0_dot(const T* row, const float* v, int hd) {
+  float acc = 0.f;
+  for (int d = 0; d < hd; d += 4) {
+    float x[4];
+    ld4<T>(row + d, x);
+    acc = fmaf(x[0], v[d], acc);
+    acc = fmaf(x[1], v[d + 1], acc);
+    acc = fmaf(x[2], v[d + 2], acc);
+    acc = fmaf(x[3], v[d + 3], acc);
+  }
+  return acc;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void attn_fwd_row0_kernel(const T* __restrict__ qkv, T* __restrict__ o,
+                                                            float* __restrict__ lse, int64_t Tn, int64_t H, int hd,
+                                                            float scale) {
+  __shared__ float q0[R0_HDMAX], pv[R0_TMAX], red[8], part[4][R0_HDMAX];
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * hd, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld;
+  r0_load_row<T>(base + h * hd, hd, q0);
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  float mloc = -INFINITY;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float s = r0_dot<T>(base + k * ld + D + h * hd, q0, hd) * c2;
+    pv[k] = s;
+    mloc = fmaxf(mloc, s);
+  }
+  const float m = r0_block_max(mloc, red);
+  float lloc = 0.f;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float p = exp2f(pv[k] - m);
+    pv[k] = p;
+    lloc += p;
+  }
+  const float l = r0_block_sum(lloc, red);              // (its barriers also publish pv)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int d0 = 0; d0 < hd; d0 += 64) {
+    const int d = d0 + lane;
+    float acc = 0.f;
+    if (d < hd)
+      for (int64_t k = w; k < Tn; k += 4) acc = fmaf(pv[k], ld1<T>(base + k * ld + 2 * D + h * hd + d), acc);
+    if (d < hd) part[w][d] = acc;
+  }
+  __syncthreads();
+  const float inv = 1.0f / l;
+  for (int d = threadIdx.x; d < hd; d += blockDim.x)
+    st1<T>(o + b * Tn * D + h * hd + d, (((part[0][d] + part[1][d]) + part[2][d]) + part[3][d]) * inv);
+  if (threadIdx.x == 0) lse[bh * Tn] = (m + log2f(l)) / LOG2E;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void attn_bwd_row0_kernel(const T* __restrict__ qkv, const T* __restrict__ d_o0,
+                                                            int64_t ldo, const float* __restrict__ lse,
+                                                            T* __restrict__ dqkv, int64_t Tn, int64_t H, int hd,
+                                                            float scale) {
+  __shared__ float q0[R0_HDMAX], g0[R0_HDMAX], ds[R0_TMAX], red[8], part[4][R0_HDMAX];
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * hd, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld;
+  T* dbase = dqkv + b * Tn * ld;
+  r0_load_row<T>(base + h * hd, hd, q0);
+  r0_load_row<T>(d_o0 + b * ldo + h * hd, hd, g0);
+  __syncthreads();
+  const float c2 = scale * LOG2E, l2 = lse[bh * Tn] * LOG2E;
+  // P_k and dP_k = dO0 . V_k; dV_k = P_k dO0 written now; delta = sum_k P_k dP_k
+  float dloc = 0.f;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float p = exp2f(r0_dot<T>(base + k * ld + D + h * hd, q0, hd) * c2 - l2);
+    const float dp = r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
+    ds[k] = p;
+    dloc = fmaf(p, dp, dloc);
+    T* dv = dbase + k * ld + 2 * D + h * hd;
+    for (int d = 0; d < hd; d += 4) {
+      const float v[4] = {p * g0[d], p * g0[d + 1], p * g0[d + 2], p * g0[d + 3]};
+      st4<T>(dv + d, v);
+    }
+    if (Tn <= R0_TMAX / 2) ds[R0_TMAX / 2 + k] = dp;   // dP_k kept until delta is known (recomputed past 2048)
+  }
+  const float delta = r0_block_sum(dloc, red);
+  // dS_k = P_k (dP_k - delta); dK_k = scale dS_k q0
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float dp = Tn <= R0_TMAX / 2 ? ds[R0_TMAX / 2 + k] : r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
+    const float s = ds[k] * (dp - delta);
+    ds[k] = s;
+    T* dk = dbase + k * ld + D + h * hd;
+    for (int d = 0; d < hd; d += 4) {
+      const float v[4] = {scale * s * q0[d], scale * s * q0[d + 1], scale * s * q0[d + 2], scale * s * q0[d + 3]};
+      st4<T>(dk + d, v);
+    }
+  }
+  __syncthreads();
+  // dQ0 = scale sum_k dS_k K_k: lanes over d, waves over keys, partials in wave order
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int d0 = 0; d0 < hd; d0 += 64) {
+    const int d = d0 + lane;
+    float acc = 0.f;
+    if (d < hd)
+      for (int64_t k = w; k < Tn; k += 4) acc = fmaf(ds[k], ld1<T>(base + k * ld + D + h * hd + d), acc);
+    if (d < hd) part[w][d] = acc;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < hd; d += blockDim.x)
+    st1<T>(dbase + h * hd + d, scale * (((part[0][d] + part[1][d]) + part[2][d]) + part[3][d]));
+}
+
 bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }
 
 }  // namespace
@@ -1639,3 +1784,38 @@ extern "C" int vit_diag_attn_istamps(unsigned long long* host, int64_t n) {
              ? 0 : 1;
 }
 #endif
+
+extern "C" int vit_attn_fwd_row0(const void* qkv, void* o, float* lse, int64_t B, int64_t T, int64_t H, int64_t hd,
+                                 float scale, int32_t dtype, void* stream) {
+  VIT_REQUIRE(qkv && o && lse && B > 0 && T > 0 && H > 0 && hd > 0, "vit_attn_fwd_row0: bad arguments");
+  VIT_REQUIRE(T <= R0_TMAX && hd <= R0_HDMAX && hd % 4 == 0, "vit_attn_fwd_row0: T <= %d, hd <= %d, hd %% 4 == 0",
+              R0_TMAX, R0_HDMAX);
+  VIT_REQUIRE(((uintptr_t)qkv) % (dtype == VIT_BF16 ? 8 : 16) == 0, "vit_attn_fwd_row0: qkv must be aligned");
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16)
+    attn_fwd_row0_kernel<bf16_t><<<(unsigned)(B * H), 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, (int)hd,
+                                                                    scale);
+  else
+    attn_fwd_row0_kernel<float><<<(unsigned)(B * H), 256, 0, s>>>((const float*)qkv, (float*)o, lse, T, H, (int)hd,
+                                                                   scale);
+  return vit::check_launch("vit_attn_fwd_row0");
+}
+
+extern "C" int vit_attn_bwd_row0(const void* qkv, const void* d_o0, int64_t ldo, const float* lse, void* dqkv,
+                                 int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype,
+                                 void* stream) {
+  VIT_REQUIRE(qkv && d_o0 && lse && dqkv && B > 0 && T > 0 && H > 0 && hd > 0 && ldo >= H * hd,
+              "vit_attn_bwd_row0: bad arguments");
+  VIT_REQUIRE(T <= R0_TMAX && hd <= R0_HDMAX && hd % 4 == 0, "vit_attn_bwd_row0: T <= %d, hd <= %d, hd %% 4 == 0",
+              R0_TMAX, R0_HDMAX);
+  VIT_REQUIRE(((uintptr_t)qkv) % (dtype == VIT_BF16 ? 8 : 16) == 0 && ((uintptr_t)dqkv) % (dtype == VIT_BF16 ? 8 : 16) == 0,
+              "vit_attn_bwd_row0: qkv / dqkv must be aligned");
+  hipStream_t s = VIT_STREAM(stream);
+  if (dtype == VIT_BF16)
+    attn_bwd_row0_kernel<bf16_t><<<(unsigned)(B * H), 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o0, ldo, lse,
+                                                                    (bf16_t*)dqkv, T, H, (int)hd, scale);
+  else
+    attn_bwd_row0_kernel<float><<<(unsigned)(B * H), 256, 0, s>>>((const float*)qkv, (const float*)d_o0, ldo, lse,
+                                                                   (float*)dqkv, T, H, (int)hd, scale);
+  return vit::check_launch("vit_attn_bwd_row0");
+}
