@@ -64,7 +64,6 @@ const char* vit_last_error(void);
  *   "gemm_tail_v2"       0: 1 runs the tile rows of a last round of 256x256 tiles at most half full that the split-K
  *                        tail does not take as 128x128 tiles (two workgroups per CU) in a second launch (measured
  *                        slower at C2: 33.0 vs 31.6 ms/step)
- *   "adamw_vec"          1: vit_adamw moves 4 elements per lane with 16-B accesses where a chunk's pointers allow
  * vit_set_option returns VIT_ERR_INVALID for an unknown name; vit_get_option returns INT64_MIN for one. */
 int vit_set_option(const char* name, int64_t value);
 int64_t vit_get_option(const char* name);
@@ -195,13 +194,14 @@ int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d
  * output gradient on row 0 only; every softmax row is independent, so row 0 alone is the same function, in O(T hd) per
  * (image, head) instead of O(T^2 hd).
  *   fwd: o[b*T][D] (row 0 of every image; other rows untouched), lse[b][h][0].
- *   bwd: from d_o0[b][D] (image b's row-0 output gradient, row stride ldo) and lse[b][h][0]: dQ row 0, every row of dK
- *        and dV into dqkv[B*T][3*D] (dQ rows 1..T-1 untouched: the caller keeps them zero).  delta = sum_k P dP is
- *        exact (fp32 P and dP).  fp32 arithmetic, outputs rounded once; hd <= 128, T <= 4096. */
+ *   bwd: from d_o0[b][D] (image b's row-0 output gradient, row stride ldo): dQ row 0, every row of dK and dV into
+ *        dqkv[B*T][3*D] (dQ rows 1..T-1 untouched).  P is recomputed as the forward forms it (row max, exp2, 1/sum;
+ *        no log-sum-exp round trip: a one-key row has P = 1, dS = 0 exactly); delta = sum_k P dP from fp32 P and dP.
+ *   fp32 arithmetic, outputs rounded once; hd <= 128, hd % 4 == 0, T <= 4096. */
 int vit_attn_fwd_row0(const void* qkv, void* o, float* lse, int64_t B, int64_t T, int64_t H, int64_t hd, float scale,
                       int32_t dtype, void* stream);
-int vit_attn_bwd_row0(const void* qkv, const void* d_o0, int64_t ldo, const float* lse, void* dqkv, int64_t B, int64_t T,
-                      int64_t H, int64_t hd, float scale, int32_t dtype, void* stream);
+int vit_attn_bwd_row0(const void* qkv, const void* d_o0, int64_t ldo, void* dqkv, int64_t B, int64_t T, int64_t H,
+                      int64_t hd, float scale, int32_t dtype, void* stream);
 
 /* ------------------------------------------------------------------------------------------------------------
  * Reductions / elementwise.

@@ -80,7 +80,7 @@ int main(void) {
   CHECK(refused(vit_attn_fwd_row0(NULL, NULL, NULL, 1, 1, 1, 64, 1.f, VIT_BF16, NULL), "vit_attn_fwd_row0"));
   CHECK(refused(vit_attn_fwd_row0(dummy, dummy, (float*)dummy, 1, 5000, 1, 64, 1.f, VIT_BF16, NULL),
                 "vit_attn_fwd_row0"));                                                 /* T > 4096 */
-  CHECK(refused(vit_attn_bwd_row0(dummy, dummy, 8, (const float*)dummy, dummy, 1, 5, 1, 64, 1.f, VIT_BF16, NULL),
+  CHECK(refused(vit_attn_bwd_row0(dummy, dummy, 8, dummy, 1, 5, 1, 64, 1.f, VIT_BF16, NULL),
                 "vit_attn_bwd_row0"));                                                 /* ldo < H * hd */
   CHECK(refused(vit_colsum_finish(NULL, 1, 1, 1, dummy, NULL, NULL, 0.f, NULL), "vit_colsum_finish"));
   CHECK(refused(vit_colsum_finish(dummy, 1, 8, 2, dummy, NULL, NULL, 0.f, NULL), "vit_colsum_finish"));

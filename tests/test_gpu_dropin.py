@@ -140,8 +140,8 @@ def test_eval_forward_and_attention_probs_vs_oracle(dtype):
     assert all(b.multi_head.attention_probs is None for b in m.transformer_encoder.blocks)
     if bf:      # probabilities come from the VALU attention kernel; the MFMA one runs without them
         assert _rel(again.cpu(), ref) < 1e-2
-    else:
-        assert torch.equal(again, logits)
+    else:       # the pruned last block runs query 0 alone without probabilities: summation order only
+        assert (again - logits).abs().max().item() < 1e-5
 
 
 @pytest.mark.parametrize("T", [197, 577])

@@ -549,12 +549,13 @@ def test_attention_fwd_bwd(dtype, hd, T, amp):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("T,hd", [(1, 64), (5, 64), (197, 64), (197, 32), (577, 64), (2500, 16)])
+@pytest.mark.parametrize("T,hd", [(1, 64), (5, 64), (197, 64), (197, 32), (577, 64), (2500, 16), (65, 128), (197, 20)])
 def test_attention_row0_fwd_bwd(dtype, T, hd):
-    """Query 0 only (vit_attn_fwd_row0 / vit_attn_bwd_row0, the pruned last block): o row 0 and lse[.., 0] equal the
+    """Query 0 only (vit_attn_fwd_row0 / vit_attn_bwd_row0, the pruned last block; hd = 20: the generic one-key-per-
+    thread kernels, the rest the lane-chunk kernels): o row 0 and lse[.., 0] equal the
     full attention's row 0; with an output gradient on row 0 only, dQ row 0 and all of dK / dV equal the full
-    backward's, and the dQ rows 1..T-1 (and o rows 1..T-1) are left untouched.  fp32 to 2e-5 of the scale (fp64
-    reference), bf16 to 1e-2 of the norm (the kernels compute in fp32 and round once)."""
+    backward's, and the dQ rows 1..T-1 (and o rows 1..T-1) are left untouched.  fp32 to 2e-5 of the largest value
+    (1e-4 for dQ0) against fp64, bf16 to 1e-2 of the norm (the kernels compute in fp32 and round once)."""
     torch.manual_seed(T + hd)
     B, H = 3, 2
     D = H * hd
@@ -584,7 +585,7 @@ def test_attention_row0_fwd_bwd(dtype, T, hd):
     o_ref.backward(d_o)
     dqkv = torch.full((B * T, 3 * D), 5.0, device=DEV, dtype=dtype)
     dqkv[:, D:] = 0
-    _ops.attn_bwd_row0(qkv, g0, D, lse, dqkv, B, T, H, hd, scale)
+    _ops.attn_bwd_row0(qkv, g0, D, dqkv, B, T, H, hd, scale)
     torch.cuda.synchronize()
     assert bool((dqkv[others, :D] == 5.0).all())                       # dQ rows 1..T-1 untouched
     gref = x.grad
@@ -593,14 +594,15 @@ def test_attention_row0_fwd_bwd(dtype, T, hd):
                       ("dV", (slice(None), slice(2 * D, 3 * D)))):
         a, r = dqkv[sel].double(), gref[sel]
         if dtype == torch.float32:
+            # dQ0 = scale sum_k dS_k K_k with sum_k dS_k = 0: a cancelling sum, gated at the fp32 parity bound (1e-4)
             err = float((a - r).abs().max()) / max(floor, float(r.abs().max()))
-            assert err <= 2e-5, (name, err)
+            assert err <= (1e-4 if name == "dQ0" else 2e-5), (name, err)
         else:
             err = float((a - r).norm() / max(float(r.norm()), floor * r.numel() ** 0.5))
             assert err < 1e-2, (name, err)
     again = torch.full_like(dqkv, 5.0)
     again[:, D:] = 0
-    _ops.attn_bwd_row0(qkv, g0, D, lse, again, B, T, H, hd, scale)
+    _ops.attn_bwd_row0(qkv, g0, D, again, B, T, H, hd, scale)
     assert torch.equal(again, dqkv)                                     # deterministic
 
 
@@ -757,34 +759,6 @@ def test_misc_kernels():
     _ops.dropout_bwd(t, y, 0.2, 4242)
     keep = dropout_keep(4242, (3000,)).to(DEV)
     assert torch.equal(y, t * keep * 1.25)
-
-
-def test_adamw_vector_path_bitwise_equals_scalar():
-    """adamw_vec (16-B accesses on aligned chunks) == one element per lane, bit for bit: aligned and misaligned
-    (offset-1 views) tensors, lengths not a multiple of 4, chunks split at 64 Ki, fp32 and bf16 shadows."""
-    torch.manual_seed(8)
-    base = torch.randn(200003, device=DEV)
-    views = [base[:70001], base[70001 + 3:70001 + 3 + 301], base[1:130001 + 1], base[4:4 + 4096]]
-    outs = []
-    for vec in (1, 0):
-        for sdt in (torch.bfloat16, torch.float32):
-            ps = [v.clone() if i != 2 else torch.cat([torch.zeros(1, device=DEV), v])[1:] for i, v in enumerate(views)]
-            gs = [torch.randn_like(p) for p in ps]
-            ms = [torch.randn_like(p) * 0.1 for p in ps]
-            vs = [torch.rand_like(p) * 0.1 for p in ps]
-            sh = [torch.empty(p.shape, dtype=sdt, device=DEV) for p in ps]
-            table, n = _ops.build_chunk_table(list(zip(ps, gs, ms, vs, sh)), DEV)
-            old = _lib.get_option("adamw_vec")
-            _lib.set_option("adamw_vec", vec)
-            try:
-                for step in range(1, 3):
-                    _ops.adamw(table, n, 1e-3, 0.9, 0.999, 1e-8, 1e-4, 1 - 0.9 ** step, 1 - 0.999 ** step, 0.5, sdt)
-                torch.cuda.synchronize()
-            finally:
-                _lib.set_option("adamw_vec", old)
-            outs.append([t.clone() for t in ps + ms + vs + sh])
-    for a, b in zip(outs[:2], outs[2:]):
-        assert all(torch.equal(x, y) for x, y in zip(a, b))
 
 
 def test_adamw_matches_torch():

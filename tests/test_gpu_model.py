@@ -285,11 +285,12 @@ def test_pruned_last_block_matches_all_rows(dtype, train):
         loss.backward()
         out.append((logits.detach().cpu(), loss.item(), _grads(m)))
     tol = 1e-4 if dtype == torch.float32 else 2e-2       # Q/K weight gradients amplify summation-order rounding
-    for a in out[:2]:
+    for i, a in enumerate(out[:2]):
+        errs = sorted((_rel(a[2][k], out[2][2][k]), k) for k in out[2][2])
+        print(f"variant {i}: logits {_rel(a[0], out[2][0]):.2e}, worst gradients {errs[-3:]}")
         assert _rel(a[0], out[2][0]) < tol
         assert abs(a[1] - out[2][1]) < tol * max(1.0, abs(out[2][1]))
-        for k in out[2][2]:
-            assert _rel(a[2][k], out[2][2][k]) < tol, (k, _rel(a[2][k], out[2][2][k]))
+        assert errs[-1][0] < tol, errs[-1]
 
 
 def test_side_stream_weight_gradients_bitwise_equal():

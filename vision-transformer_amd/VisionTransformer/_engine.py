@@ -786,7 +786,7 @@ class Engine:
             # wgrad GEMMs below
             dqkv = self._token_rows("dqkv", M, 3 * D, dt, T, dev)
             mk("attn_bwd", 0, 10.0 * B * H * T * hd, 4 * M * D * es + 4 * B * D * es + 4 * B * H)
-            _ops.attn_bwd_row0(qkv, do, D, lse, dqkv, B, T, H, hd, self.scale)
+            _ops.attn_bwd_row0(qkv, do, D, dqkv, B, T, H, hd, self.scale)
             mk("attn_bwd", 1)
         else:
             if pr:

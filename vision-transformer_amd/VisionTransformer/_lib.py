@@ -74,7 +74,7 @@ _SIGS = {
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
     "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _I32, _P]),
     "vit_attn_fwd_row0": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
-    "vit_attn_bwd_row0": (ctypes.c_int, [_P, _P, _I64, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
+    "vit_attn_bwd_row0": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
     "vit_colsum_workspace_bytes": (_I64, [_I64, _I64]),
     "vit_colsum": (ctypes.c_int, [_P, _I64, _I32, _I64, _I64, _P, _F, _F, _P, _P]),
     "vit_colsum_finish": (ctypes.c_int, [_P, _I64, _I64, _I32, _P, _P, _P, _F, _P]),

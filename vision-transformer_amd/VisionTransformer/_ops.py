@@ -212,11 +212,11 @@ def attn_fwd_row0(qkv, B, T, H, hd, scale, o=None, lse=None, stream=None):
     return o, lse
 
 
-def attn_bwd_row0(qkv, d_o0, ldo, lse, dqkv, B, T, H, hd, scale, stream=None):
+def attn_bwd_row0(qkv, d_o0, ldo, dqkv, B, T, H, hd, scale, stream=None):
     """Backward of attn_fwd_row0 from the row-0 output gradients d_o0 (image b at row b, stride ldo): dQ row 0 and all
     of dK, dV into dqkv (dQ rows 1..T-1 untouched)."""
-    _need_cuda(qkv, d_o0, lse, dqkv)
-    _lib.call("vit_attn_bwd_row0", _ptr(qkv), _ptr(d_o0), ldo, _ptr(lse), _ptr(dqkv), B, T, H, hd, scale,
+    _need_cuda(qkv, d_o0, dqkv)
+    _lib.call("vit_attn_bwd_row0", _ptr(qkv), _ptr(d_o0), ldo, _ptr(dqkv), B, T, H, hd, scale,
               dtype_code(qkv), _stream(stream))
     return dqkv
 

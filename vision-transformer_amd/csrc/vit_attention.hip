@@ -1594,23 +1594,41 @@ __global__ __launch_bounds__(256) void attn_fwd_row0_kernel(const T* __restrict_
 
 template <class T>
 __global__ __launch_bounds__(256) void attn_bwd_row0_kernel(const T* __restrict__ qkv, const T* __restrict__ d_o0,
-                                                            int64_t ldo, const float* __restrict__ lse,
-                                                            T* __restrict__ dqkv, int64_t Tn, int64_t H, int hd,
-                                                            float scale) {
+                                                            int64_t ldo, T* __restrict__ dqkv, int64_t Tn, int64_t H,
+                                                            int hd, float scale) {
+  // ds[0 .. T): scores, then P, then dS; ds[R0_TMAX/2 + k]: dP_k while T <= R0_TMAX / 2 (recomputed past that)
   __shared__ float q0[R0_HDMAX], g0[R0_HDMAX], ds[R0_TMAX], red[8], part[4][R0_HDMAX];
   const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
   const int64_t D = H * hd, ld = 3 * D;
   const T* base = qkv + b * Tn * ld;
   T* dbase = dqkv + b * Tn * ld;
+  const bool keep_dp = Tn <= R0_TMAX / 2;
   r0_load_row<T>(base + h * hd, hd, q0);
   r0_load_row<T>(d_o0 + b * ldo + h * hd, hd, g0);
   __syncthreads();
-  const float c2 = scale * LOG2E, l2 = lse[bh * Tn] * LOG2E;
-  // P_k and dP_k = dO0 . V_k; dV_k = P_k dO0 written now; delta = sum_k P_k dP_k
+  // P recomputed exactly as the forward forms it (max, exp2, 1/sum): no log-sum-exp round trip, so a one-key row
+  // has P = 1 and dS = 0 exactly
+  const float c2 = scale * LOG2E;
+  float mloc = -INFINITY;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float sk = r0_dot<T>(base + k * ld + D + h * hd, q0, hd) * c2;
+    ds[k] = sk;
+    mloc = fmaxf(mloc, sk);
+    if (keep_dp) ds[R0_TMAX / 2 + k] = r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
+  }
+  const float m = r0_block_max(mloc, red);
+  float lloc = 0.f;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float p = exp2f(ds[k] - m);
+    ds[k] = p;
+    lloc += p;
+  }
+  const float inv = 1.0f / r0_block_sum(lloc, red);
+  // P_k = p_k / l; dV_k = P_k dO0; delta = sum_k P_k dP_k
   float dloc = 0.f;
   for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
-    const float p = exp2f(r0_dot<T>(base + k * ld + D + h * hd, q0, hd) * c2 - l2);
-    const float dp = r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
+    const float p = ds[k] * inv;
+    const float dp = keep_dp ? ds[R0_TMAX / 2 + k] : r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
     ds[k] = p;
     dloc = fmaf(p, dp, dloc);
     T* dv = dbase + k * ld + 2 * D + h * hd;
@@ -1618,17 +1636,16 @@ __global__ __launch_bounds__(256) void attn_bwd_row0_kernel(const T* __restrict_
       const float v[4] = {p * g0[d], p * g0[d + 1], p * g0[d + 2], p * g0[d + 3]};
       st4<T>(dv + d, v);
     }
-    if (Tn <= R0_TMAX / 2) ds[R0_TMAX / 2 + k] = dp;   // dP_k kept until delta is known (recomputed past 2048)
   }
   const float delta = r0_block_sum(dloc, red);
   // dS_k = P_k (dP_k - delta); dK_k = scale dS_k q0
   for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
-    const float dp = Tn <= R0_TMAX / 2 ? ds[R0_TMAX / 2 + k] : r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
-    const float s = ds[k] * (dp - delta);
-    ds[k] = s;
+    const float dp = keep_dp ? ds[R0_TMAX / 2 + k] : r0_dot<T>(base + k * ld + 2 * D + h * hd, g0, hd);
+    const float sk = ds[k] * (dp - delta);
+    ds[k] = sk;
     T* dk = dbase + k * ld + D + h * hd;
     for (int d = 0; d < hd; d += 4) {
-      const float v[4] = {scale * s * q0[d], scale * s * q0[d + 1], scale * s * q0[d + 2], scale * s * q0[d + 3]};
+      const float v[4] = {scale * sk * q0[d], scale * sk * q0[d + 1], scale * sk * q0[d + 2], scale * sk * q0[d + 3]};
       st4<T>(dk + d, v);
     }
   }
@@ -1645,6 +1662,214 @@ __global__ __launch_bounds__(256) void attn_bwd_row0_kernel(const T* __restrict_
   __syncthreads();
   for (int d = threadIdx.x; d < hd; d += blockDim.x)
     st1<T>(dbase + h * hd + d, scale * (((part[0][d] + part[1][d]) + part[2][d]) + part[3][d]));
+}
+
+// The same two functions with the head dimension on the lanes: LPK lanes per key, one 16-B chunk each, so a wave
+// reads KPW = 64 / LPK whole 16-B-aligned key rows per instruction (the kernels above give each thread a key: 64 rows
+// 4.6 KB apart per load, address-bound).  Dot products: each lane's chunk in order, then a fixed xor tree over the
+// LPK lanes; value-weighted sums: per lane over its keys, a fixed xor tree over the wave's key slots, waves in order.
+template <class T> struct R0Chunk;
+template <> struct R0Chunk<bf16_t> {
+  static constexpr int CH = 8;
+  static VIT_DEV void ld(const bf16_t* p, float* x) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = __uint_as_float(w[i] << 16);
+      x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static VIT_DEV void st(bf16_t* p, const float* x) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(x[0]) | ((uint32_t)f2bf(x[1]) << 16);
+    u.y = (uint32_t)f2bf(x[2]) | ((uint32_t)f2bf(x[3]) << 16);
+    u.z = (uint32_t)f2bf(x[4]) | ((uint32_t)f2bf(x[5]) << 16);
+    u.w = (uint32_t)f2bf(x[6]) | ((uint32_t)f2bf(x[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+};
+template <> struct R0Chunk<float> {
+  static constexpr int CH = 4;
+  static VIT_DEV void ld(const float* p, float* x) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p);
+    x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
+  }
+  static VIT_DEV void st(float* p, const float* x) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{x[0], x[1], x[2], x[3]};
+  }
+};
+
+template <int LPK>
+VIT_DEV float r0_lane_sum(float v) {          // over the LPK lanes of one key (all of them get the sum)
+#pragma unroll
+  for (int off = LPK / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// acc[CH] summed over the wave's key slots (lanes with the same chunk), then over the 4 waves in order -> out[hd]
+template <int LPK, int CH>
+VIT_DEV void r0_slot_reduce(float* acc, float (*part)[R0_HDMAX], float* out_lds) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = LPK; off < 64; off <<= 1)
+#pragma unroll
+    for (int j = 0; j < CH; ++j) acc[j] += __shfl_xor(acc[j], off, 64);
+  if (lane < LPK)
+#pragma unroll
+    for (int j = 0; j < CH; ++j) part[w][lane * CH + j] = acc[j];
+  __syncthreads();
+  for (int d = threadIdx.x; d < LPK * CH; d += blockDim.x)
+    out_lds[d] = ((part[0][d] + part[1][d]) + part[2][d]) + part[3][d];
+}
+
+template <class T, int LPK>
+__global__ __launch_bounds__(256) void attn_fwd_row0_vec(const T* __restrict__ qkv, T* __restrict__ o,
+                                                         float* __restrict__ lse, int64_t Tn, int64_t H, float scale) {
+  constexpr int CH = R0Chunk<T>::CH, HDc = LPK * CH, KPW = 64 / LPK, KPB = 4 * KPW;
+  __shared__ float sc[R0_TMAX], red[8], part[4][R0_HDMAX], res[R0_HDMAX];
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * HDc, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld + h * HDc;
+  const int lane = threadIdx.x & 63, c = lane % LPK, slot = (threadIdx.x >> 6) * KPW + lane / LPK;
+  float q[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) q[j] = ld1<T>(base + c * CH + j);
+  const float c2 = scale * LOG2E;
+  float mloc = -INFINITY;
+  for (int64_t k0 = 0; k0 < Tn; k0 += KPB) {
+    const int64_t k = k0 + slot;
+    float x[CH];
+    float d = 0.f;
+    if (k < Tn) {
+      R0Chunk<T>::ld(base + k * ld + D + c * CH, x);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) d = fmaf(x[j], q[j], d);
+    }
+    d = r0_lane_sum<LPK>(d) * c2;
+    if (k < Tn) {
+      if (c == 0) sc[k] = d;
+      mloc = fmaxf(mloc, d);
+    }
+  }
+  const float m = r0_block_max(mloc, red);               // (its barriers also publish sc)
+  float lloc = 0.f;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float p = exp2f(sc[k] - m);
+    sc[k] = p;
+    lloc += p;
+  }
+  const float l = r0_block_sum(lloc, red);
+  float acc[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) acc[j] = 0.f;
+  for (int64_t k0 = 0; k0 < Tn; k0 += KPB) {
+    const int64_t k = k0 + slot;
+    if (k < Tn) {
+      float x[CH];
+      R0Chunk<T>::ld(base + k * ld + 2 * D + c * CH, x);
+      const float p = sc[k];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) acc[j] = fmaf(p, x[j], acc[j]);
+    }
+  }
+  r0_slot_reduce<LPK, CH>(acc, part, res);
+  __syncthreads();
+  const float inv = 1.0f / l;
+  for (int d = threadIdx.x; d < HDc; d += blockDim.x) st1<T>(o + b * Tn * D + h * HDc + d, res[d] * inv);
+  if (threadIdx.x == 0) lse[bh * Tn] = (m + log2f(l)) / LOG2E;
+}
+
+template <class T, int LPK>
+__global__ __launch_bounds__(256) void attn_bwd_row0_vec(const T* __restrict__ qkv, const T* __restrict__ d_o0,
+                                                         int64_t ldo, T* __restrict__ dqkv, int64_t Tn, int64_t H,
+                                                         float scale) {
+  constexpr int CH = R0Chunk<T>::CH, HDc = LPK * CH, KPW = 64 / LPK, KPB = 4 * KPW;
+  __shared__ float sc[R0_TMAX], dpv[R0_TMAX], red[8], part[4][R0_HDMAX], res[R0_HDMAX];
+  const int64_t bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int64_t D = H * HDc, ld = 3 * D;
+  const T* base = qkv + b * Tn * ld + h * HDc;
+  T* dbase = dqkv + b * Tn * ld + h * HDc;
+  const int lane = threadIdx.x & 63, c = lane % LPK, slot = (threadIdx.x >> 6) * KPW + lane / LPK;
+  float q[CH], g[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) {
+    q[j] = ld1<T>(base + c * CH + j);
+    g[j] = ld1<T>(d_o0 + b * ldo + h * HDc + c * CH + j);
+  }
+  // scores and dP_k = dO0 . V_k; P recomputed as the forward forms it (row max, exp2, 1/sum)
+  const float c2 = scale * LOG2E;
+  float mloc = -INFINITY;
+  for (int64_t k0 = 0; k0 < Tn; k0 += KPB) {
+    const int64_t k = k0 + slot;
+    float sd = 0.f, pd = 0.f;
+    if (k < Tn) {
+      float x[CH], y[CH];
+      R0Chunk<T>::ld(base + k * ld + D + c * CH, x);
+      R0Chunk<T>::ld(base + k * ld + 2 * D + c * CH, y);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        sd = fmaf(x[j], q[j], sd);
+        pd = fmaf(y[j], g[j], pd);
+      }
+    }
+    sd = r0_lane_sum<LPK>(sd) * c2;
+    pd = r0_lane_sum<LPK>(pd);
+    if (k < Tn) {
+      if (c == 0) {
+        sc[k] = sd;
+        dpv[k] = pd;
+      }
+      mloc = fmaxf(mloc, sd);
+    }
+  }
+  const float m = r0_block_max(mloc, red);
+  float lloc = 0.f;
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float p = exp2f(sc[k] - m);
+    sc[k] = p;
+    lloc += p;
+  }
+  const float inv = 1.0f / r0_block_sum(lloc, red);
+  float dloc = 0.f;                                       // delta = sum_k P_k dP_k
+  for (int64_t k = threadIdx.x; k < Tn; k += blockDim.x) {
+    const float p = sc[k] * inv;
+    sc[k] = p;
+    dloc = fmaf(p, dpv[k], dloc);
+  }
+  const float delta = r0_block_sum(dloc, red);
+  // per key: dV_k = P_k dO0, dS_k = P_k (dP_k - delta), dK_k = scale dS_k q0; dQ0 = scale sum_k dS_k K_k
+  float acc[CH];
+#pragma unroll
+  for (int j = 0; j < CH; ++j) acc[j] = 0.f;
+  for (int64_t k0 = 0; k0 < Tn; k0 += KPB) {
+    const int64_t k = k0 + slot;
+    if (k < Tn) {
+      const float p = sc[k];
+      const float ds = p * (dpv[k] - delta), f = scale * ds;
+      float x[CH], v[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) v[j] = p * g[j];
+      R0Chunk<T>::st(dbase + k * ld + 2 * D + c * CH, v);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) v[j] = f * q[j];
+      R0Chunk<T>::st(dbase + k * ld + D + c * CH, v);
+      R0Chunk<T>::ld(base + k * ld + D + c * CH, x);
+#pragma unroll
+      for (int j = 0; j < CH; ++j) acc[j] = fmaf(ds, x[j], acc[j]);
+    }
+  }
+  r0_slot_reduce<LPK, CH>(acc, part, res);
+  __syncthreads();
+  for (int d = threadIdx.x; d < HDc; d += blockDim.x) st1<T>(dbase + d, scale * res[d]);
+}
+
+// lanes per key for the lane-chunk kernels: hd / (16 B / element), a power of two <= 64; 0: the generic kernels
+int r0_lpk(int32_t dtype, int64_t hd, const void* p0, const void* p1) {
+  const int ch = dtype == VIT_BF16 ? 8 : 4;
+  if (hd % ch != 0 || ((uintptr_t)p0 | (uintptr_t)p1) % 16 != 0) return 0;
+  const int64_t lpk = hd / ch;
+  return (lpk & (lpk - 1)) == 0 && lpk <= 64 ? (int)lpk : 0;
 }
 
 bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD; }
@@ -1792,6 +2017,16 @@ extern "C" int vit_attn_fwd_row0(const void* qkv, void* o, float* lse, int64_t B
               R0_TMAX, R0_HDMAX);
   VIT_REQUIRE(((uintptr_t)qkv) % (dtype == VIT_BF16 ? 8 : 16) == 0, "vit_attn_fwd_row0: qkv must be aligned");
   hipStream_t s = VIT_STREAM(stream);
+  const unsigned grid = (unsigned)(B * H);
+  switch (r0_lpk(dtype, hd, qkv, qkv) * (dtype == VIT_BF16 ? 1 : -1)) {
+#define R0F(L, TT) attn_fwd_row0_vec<TT, L><<<grid, 256, 0, s>>>((const TT*)qkv, (TT*)o, lse, T, H, scale); \
+  return vit::check_launch("vit_attn_fwd_row0")
+    case 1: R0F(1, bf16_t);   case 2: R0F(2, bf16_t);   case 4: R0F(4, bf16_t);  case 8: R0F(8, bf16_t);
+    case 16: R0F(16, bf16_t); case -1: R0F(1, float);   case -2: R0F(2, float);  case -4: R0F(4, float);
+    case -8: R0F(8, float);   case -16: R0F(16, float); case -32: R0F(32, float);
+#undef R0F
+    default: break;
+  }
   if (dtype == VIT_BF16)
     attn_fwd_row0_kernel<bf16_t><<<(unsigned)(B * H), 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, lse, T, H, (int)hd,
                                                                     scale);
@@ -1801,21 +2036,32 @@ extern "C" int vit_attn_fwd_row0(const void* qkv, void* o, float* lse, int64_t B
   return vit::check_launch("vit_attn_fwd_row0");
 }
 
-extern "C" int vit_attn_bwd_row0(const void* qkv, const void* d_o0, int64_t ldo, const float* lse, void* dqkv,
+extern "C" int vit_attn_bwd_row0(const void* qkv, const void* d_o0, int64_t ldo, void* dqkv,
                                  int64_t B, int64_t T, int64_t H, int64_t hd, float scale, int32_t dtype,
                                  void* stream) {
-  VIT_REQUIRE(qkv && d_o0 && lse && dqkv && B > 0 && T > 0 && H > 0 && hd > 0 && ldo >= H * hd,
+  VIT_REQUIRE(qkv && d_o0 && dqkv && B > 0 && T > 0 && H > 0 && hd > 0 && ldo >= H * hd,
               "vit_attn_bwd_row0: bad arguments");
   VIT_REQUIRE(T <= R0_TMAX && hd <= R0_HDMAX && hd % 4 == 0, "vit_attn_bwd_row0: T <= %d, hd <= %d, hd %% 4 == 0",
               R0_TMAX, R0_HDMAX);
   VIT_REQUIRE(((uintptr_t)qkv) % (dtype == VIT_BF16 ? 8 : 16) == 0 && ((uintptr_t)dqkv) % (dtype == VIT_BF16 ? 8 : 16) == 0,
               "vit_attn_bwd_row0: qkv / dqkv must be aligned");
   hipStream_t s = VIT_STREAM(stream);
+  const unsigned grid = (unsigned)(B * H);
+  switch (r0_lpk(dtype, hd, qkv, dqkv) * (dtype == VIT_BF16 ? 1 : -1)) {
+#define R0B(L, TT) attn_bwd_row0_vec<TT, L><<<grid, 256, 0, s>>>((const TT*)qkv, (const TT*)d_o0, ldo, (TT*)dqkv, T, \
+                                                              H, scale); \
+  return vit::check_launch("vit_attn_bwd_row0")
+    case 1: R0B(1, bf16_t);   case 2: R0B(2, bf16_t);   case 4: R0B(4, bf16_t);  case 8: R0B(8, bf16_t);
+    case 16: R0B(16, bf16_t); case -1: R0B(1, float);   case -2: R0B(2, float);  case -4: R0B(4, float);
+    case -8: R0B(8, float);   case -16: R0B(16, float); case -32: R0B(32, float);
+#undef R0B
+    default: break;
+  }
   if (dtype == VIT_BF16)
-    attn_bwd_row0_kernel<bf16_t><<<(unsigned)(B * H), 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o0, ldo, lse,
+    attn_bwd_row0_kernel<bf16_t><<<(unsigned)(B * H), 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o0, ldo,
                                                                     (bf16_t*)dqkv, T, H, (int)hd, scale);
   else
-    attn_bwd_row0_kernel<float><<<(unsigned)(B * H), 256, 0, s>>>((const float*)qkv, (const float*)d_o0, ldo, lse,
+    attn_bwd_row0_kernel<float><<<(unsigned)(B * H), 256, 0, s>>>((const float*)qkv, (const float*)d_o0, ldo,
                                                                    (float*)dqkv, T, H, (int)hd, scale);
   return vit::check_launch("vit_attn_bwd_row0");
 }

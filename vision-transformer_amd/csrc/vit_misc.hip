@@ -42,9 +42,9 @@ constexpr OptDef kOpts[vit::OPT_COUNT] = {
     {"gemm_impl", 0},        {"gemm_tail", 1},          {"gemm_tail_min_kt", 32}, {"splitk_min_kt", 0},
     {"gemm_group_m", 0},     {"gemm_epi_general", 0},   {"gemm_persist", 1},      {"attn_fwd_split", 0},
     {"attn_bwd_split", 0},   {"attn_bwd_grid", 0},      {"ln16", 1},              {"ln_al", 1},
-    {"attn_fwd_ring", 1},    {"gemm_tail_v2", 0},    {"adamw_vec", 1},
+    {"attn_fwd_ring", 1},    {"gemm_tail_v2", 0},
 };
-std::atomic<int64_t> g_opt[vit::OPT_COUNT] = {0, 1, 32, 0, 0, 0, 1, 0, 0, 0, 1, 1, 1, 0, 1};
+std::atomic<int64_t> g_opt[vit::OPT_COUNT] = {0, 1, 32, 0, 0, 0, 1, 0, 0, 0, 1, 1, 1, 0};
 
 int opt_index(const char* name) {
   if (!name) return -1;
@@ -337,55 +337,22 @@ __global__ __launch_bounds__(256) void xent_reduce_kernel(const float* __restric
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Multi-tensor AdamW: one workgroup per table chunk (<= 64 Ki elements).  Chunks whose p / g / m / v start 16-B
-// aligned (and the shadow 4-element aligned) run 4 elements per lane per step with 16-B loads and stores; the rest
-// (and the last n % 4 elements) one per lane.  Same per-element arithmetic either way.
+// Multi-tensor AdamW: one workgroup per table chunk (<= 64 Ki elements), 4 elements per lane per step.
 // ---------------------------------------------------------------------------------------------------------------
-struct AdamWArgs {
-  float decay, b1, b2, eps, step_size, inv_sqrt_bc2, gscale;
-};
-
-VIT_DEV float adamw_one(float g, float& m, float& v, float p, const AdamWArgs& a) {
-  g *= a.gscale;
-  p *= a.decay;
-  m = a.b1 * m + (1.0f - a.b1) * g;
-  v = a.b2 * v + (1.0f - a.b2) * g * g;
-  const float denom = sqrtf(v) * a.inv_sqrt_bc2 + a.eps;
-  return p - a.step_size * (m / denom);
-}
-
 template <class TS>
 __global__ __launch_bounds__(256) void adamw_kernel(const vit_tensor_chunk* __restrict__ tab, float lr, float b1,
                                                     float b2, float eps, float wd, float step_size,
-                                                    float inv_sqrt_bc2, float gscale, int vec) {
+                                                    float inv_sqrt_bc2, float gscale) {
   const vit_tensor_chunk ch = tab[blockIdx.x];
-  const AdamWArgs a{1.0f - lr * wd, b1, b2, eps, step_size, inv_sqrt_bc2, gscale};
-  int64_t t0 = 0;
-  const uintptr_t al = (uintptr_t)ch.p | (uintptr_t)ch.g | (uintptr_t)ch.m | (uintptr_t)ch.v;
-  if (vec && al % 16 == 0 && (uintptr_t)ch.shadow % (4 * sizeof(TS)) == 0) {
-    const int64_t n4 = ch.n >> 2;
-    for (int64_t i = threadIdx.x; i < n4; i += 256) {
-      const f32x4 g = __builtin_nontemporal_load((const f32x4*)ch.g + i);
-      f32x4 m = ((const f32x4*)ch.m)[i], v = ((const f32x4*)ch.v)[i], p = ((const f32x4*)ch.p)[i];
-      float q[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float mj = m[j], vj = v[j];
-        q[j] = adamw_one(g[j], mj, vj, p[j], a);
-        m[j] = mj;
-        v[j] = vj;
-        p[j] = q[j];
-      }
-      ((f32x4*)ch.m)[i] = m;
-      ((f32x4*)ch.v)[i] = v;
-      ((f32x4*)ch.p)[i] = p;
-      if (ch.shadow) st4<TS>((TS*)ch.shadow + 4 * i, q);
-    }
-    t0 = n4 << 2;
-  }
-  for (int64_t t = t0 + threadIdx.x; t < ch.n; t += 256) {
-    float m = ch.m[t], v = ch.v[t];
-    const float p = adamw_one(ch.g[t], m, v, ch.p[t], a);
+  const float decay = 1.0f - lr * wd;
+  for (int64_t t = threadIdx.x; t < ch.n; t += 256) {
+    float g = ch.g[t] * gscale;
+    float m = ch.m[t], v = ch.v[t], p = ch.p[t];
+    p *= decay;
+    m = b1 * m + (1.0f - b1) * g;
+    v = b2 * v + (1.0f - b2) * g * g;
+    const float denom = sqrtf(v) * inv_sqrt_bc2 + eps;
+    p -= step_size * (m / denom);
     ch.m[t] = m;
     ch.v[t] = v;
     ch.p[t] = p;
@@ -600,14 +567,13 @@ extern "C" int vit_adamw(const vit_tensor_chunk* table_dev, int64_t nchunks, flo
   VIT_REQUIRE(table_dev && nchunks > 0 && bias_corr1 > 0.f && bias_corr2 > 0.f, "vit_adamw: bad arguments");
   const float step_size = lr / bias_corr1;
   const float inv_sqrt_bc2 = 1.0f / sqrtf(bias_corr2);
-  const int vec = (int)vit::opt(vit::OPT_ADAMW_VEC);
   hipStream_t s = VIT_STREAM(stream);
   if (shadow_dtype == VIT_BF16)
     adamw_kernel<bf16_t><<<(unsigned)nchunks, 256, 0, s>>>(table_dev, lr, beta1, beta2, eps, weight_decay, step_size,
-                                                           inv_sqrt_bc2, grad_scale, vec);
+                                                           inv_sqrt_bc2, grad_scale);
   else
     adamw_kernel<float><<<(unsigned)nchunks, 256, 0, s>>>(table_dev, lr, beta1, beta2, eps, weight_decay, step_size,
-                                                          inv_sqrt_bc2, grad_scale, vec);
+                                                          inv_sqrt_bc2, grad_scale);
   return vit::check_launch("vit_adamw");
 }
 
