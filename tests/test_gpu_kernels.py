@@ -737,6 +737,19 @@ def test_misc_kernels():
     dst = torch.ones(4 * 3, 8, device=DEV)
     _ops.copy2d(src, 8, dst, 8, 12, 8, group=(3, 5), beta=1.0)
     assert torch.allclose(dst, src.view(4, 5, 8)[:, :3].reshape(12, 8) + 1)
+    # the 16-B raw path (same dtype, no beta, aligned): bit-exact, grouped rows (the patch-gradient gather), strided
+    # rows, and an unaligned leading dimension that must take the element path
+    for dt in (torch.bfloat16, torch.float32):
+        src = torch.randn(6 * 197, 776, device=DEV).to(dt)
+        dst = torch.zeros(6 * 196, 768, device=DEV, dtype=dt)
+        _ops.copy2d(src, 776, dst, 768, 6 * 196, 768, group=(196, 197))
+        assert torch.equal(dst, src.view(6, 197, 776)[:, :196, :768].reshape(6 * 196, 768))
+        d2 = torch.zeros(6, 768 + 4, device=DEV, dtype=dt)
+        _ops.copy2d(src, 197 * 776, d2, 768 + 4, 6, 768)
+        assert torch.equal(d2[:, :768], src.view(6, 197, 776)[:, 0, :768]) and bool((d2[:, 768:] == 0).all())
+        d3 = torch.zeros(5, 12, device=DEV, dtype=dt)
+        _ops.copy2d(src, 3, d3, 12, 5, 12)
+        assert torch.equal(d3, torch.as_strided(src, (5, 12), (3, 1)))
     # GELU
     z = torch.randn(5000, device=DEV) * 3
     assert (_ops.gelu_fwd(z) - torch.nn.functional.gelu(z)).abs().max().item() < 1e-5

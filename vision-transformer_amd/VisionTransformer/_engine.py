@@ -79,10 +79,11 @@ def split_k_for(m, n, k, dtype=torch.bfloat16):
 
 def head_split_for(m, n, k):
     """K split for the classifier head's fp32 GEMMs (M = batch rows only): ~1024 workgroups of the 64x64 fp32
-    tile, each slice >= 8 k-steps of 16.  Without it these few-tile GEMMs run one long dependent k-loop per CU."""
+    tile, each slice >= 4 k-steps of 32 (128 k).  Without it these few-tile GEMMs run one long dependent k-loop per
+    CU."""
     tiles = ((m + 63) // 64) * ((n + 63) // 64)
-    nkt = (k + 15) // 16
-    return max(1, min((1024 + tiles - 1) // tiles, nkt // 8, 32))
+    nkt = (k + 31) // 32
+    return max(1, min((1024 + tiles - 1) // tiles, nkt // 4, 32))
 
 
 class Tape:

@@ -1429,21 +1429,29 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v4(GemmArgs g, EpiParams e, 
 // ------------------------------------------------------------------------------------------------------------
 // f32 MFMA kernel (exact fp32; generic strides; any M/N/K)
 // ------------------------------------------------------------------------------------------------------------
-constexpr int FBM = 64, FBK = 16, FPAD = 4;
+constexpr int FBM = 64, FBK = 32, FPAD = 4, FLD = FBM * FBK / 256;   // FLD: elements per thread per operand tile
 
+// One k-tile of an operand into registers (the next tile is fetched while the current one's MFMAs run)
 template <bool KC>
-VIT_DEV void f32_load_stage(const float* __restrict__ src, int64_t ld, int64_t rows, int64_t K, int64_t r0,
-                            int64_t k0, int tid, float (*S)[FBM + FPAD]) {
+VIT_DEV void f32_fetch(const float* __restrict__ src, int64_t ld, int64_t rows, int64_t K, int64_t r0, int64_t k0,
+                       int tid, float (&v)[FLD]) {
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < FLD; ++it) {
     const int q = tid + 256 * it;
     int ii, rr;
-    if (KC) { ii = q >> 4; rr = q & 15; }
-    else { rr = q >> 6; ii = q & 63; }
+    if (KC) { ii = q / FBK; rr = q % FBK; }
+    else { rr = q / FBM; ii = q % FBM; }
     const int64_t gi = r0 + ii, gk = k0 + rr;
-    float v = 0.f;
-    if (gi < rows && gk < K) v = KC ? src[gi * ld + gk] : src[gk * ld + gi];
-    S[rr][ii] = v;
+    v[it] = (gi < rows && gk < K) ? (KC ? src[gi * ld + gk] : src[gk * ld + gi]) : 0.f;
+  }
+}
+template <bool KC>
+VIT_DEV void f32_put(int tid, const float (&v)[FLD], float (*S)[FBM + FPAD]) {
+#pragma unroll
+  for (int it = 0; it < FLD; ++it) {
+    const int q = tid + 256 * it;
+    if (KC) S[q % FBK][q / FBK] = v[it];
+    else S[q / FBM][q % FBM] = v[it];
   }
 }
 
@@ -1462,10 +1470,19 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g, EpiParams e) 
   const float* A = (const float*)g.a;
   const float* B = (const float*)g.b;
   f32x16 acc = {};
+  float ra[FLD], rb[FLD];
+  if (kt0 < kt1) {
+    f32_fetch<AKC>(A, g.lda, g.M, g.K, i0, kt0 * FBK, tid, ra);
+    f32_fetch<BKC>(B, g.ldb, g.N, g.K, j0, kt0 * FBK, tid, rb);
+  }
   for (int64_t kt = kt0; kt < kt1; ++kt) {
-    f32_load_stage<AKC>(A, g.lda, g.M, g.K, i0, kt * FBK, tid, Xs);
-    f32_load_stage<BKC>(B, g.ldb, g.N, g.K, j0, kt * FBK, tid, Ws);
+    f32_put<AKC>(tid, ra, Xs);
+    f32_put<BKC>(tid, rb, Ws);
     __syncthreads();
+    if (kt + 1 < kt1) {
+      f32_fetch<AKC>(A, g.lda, g.M, g.K, i0, (kt + 1) * FBK, tid, ra);
+      f32_fetch<BKC>(B, g.ldb, g.N, g.K, j0, (kt + 1) * FBK, tid, rb);
+    }
 #pragma unroll
     for (int kk = 0; kk < FBK / 2; ++kk) {
       const float a_op = Ws[2 * kk + (lane >> 5)][wn * 32 + (lane & 31)];

@@ -251,6 +251,18 @@ __global__ __launch_bounds__(256) void copy2d_kernel(const TS* __restrict__ src,
   }
 }
 
+// Same-dtype copy without beta as 16-B chunks (bit-exact; rows and leading dimensions 16-B aligned)
+__global__ __launch_bounds__(256) void copy2d_raw16_kernel(const uint8_t* __restrict__ src, int64_t lds,
+                                                           uint8_t* __restrict__ dst, int64_t ldd, int64_t rows,
+                                                           int64_t cpr, int64_t grp, int64_t grp_stride) {
+  const int64_t total = rows * cpr;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / cpr, j = (t - i * cpr) * 16;
+    const int64_t si = grp ? (i / grp) * grp_stride + (i % grp) : i;
+    *reinterpret_cast<uint4*>(dst + i * ldd + j) = *reinterpret_cast<const uint4*>(src + si * lds + j);
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void dropout_bwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n,
                                                           uint32_t thr, float scale, uint32_t seed) {  // y = keep*x*scale
@@ -488,8 +500,16 @@ extern "C" int vit_copy2d(const void* src, int64_t lds, int32_t src_dtype, void*
                           int64_t rows, int64_t cols, int64_t src_group_rows, int64_t src_group_stride, float beta,
                           void* stream) {
   VIT_REQUIRE(src && dst && rows > 0 && cols > 0, "vit_copy2d: bad arguments");
-  const unsigned grid = grid_for(rows * cols, 256, 16384);
   hipStream_t s = VIT_STREAM(stream);
+  const int64_t es = src_dtype == VIT_F32 ? 4 : 2;
+  if (src_dtype == dst_dtype && beta == 0.f && (cols * es) % 16 == 0 && (lds * es) % 16 == 0 && (ldd * es) % 16 == 0 &&
+      ((uintptr_t)src | (uintptr_t)dst) % 16 == 0) {
+    const int64_t cpr = cols * es / 16;
+    copy2d_raw16_kernel<<<grid_for(rows * cpr, 256, 16384), 256, 0, s>>>(
+        (const uint8_t*)src, lds * es, (uint8_t*)dst, ldd * es, rows, cpr, src_group_rows, src_group_stride);
+    return vit::check_launch("vit_copy2d");
+  }
+  const unsigned grid = grid_for(rows * cols, 256, 16384);
 #define CP(TS, TD)                                                                                            \
   copy2d_kernel<TS, TD><<<grid, 256, 0, s>>>((const TS*)src, lds, (TD*)dst, ldd, rows, cols, src_group_rows, \
                                              src_group_stride, beta)
