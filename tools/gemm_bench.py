@@ -7,7 +7,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "vision-transformer_amd"))
 import torch  # noqa: E402
-from VisionTransformer import _ops  # noqa: E402
+from VisionTransformer import _lib, _ops  # noqa: E402
 
 M, D = 256 * 197, 768
 SHAPES = [  # name, m, n, k, a_kcontig, b_kcontig  (C = A(i,r) B(j,r))
@@ -58,7 +58,7 @@ def main():
         outs = {}
         for rep in range(args.reps + 2):
             for impl in impls:
-                os.environ["VIT_GEMM_IMPL"] = impl
+                _lib.set_option("gemm_impl", int(impl))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 _ops.gemm(a, b, c, m, n, k, a.stride(0), b.stride(0), n, a_kcontig=akc, b_kcontig=bkc,

@@ -129,9 +129,10 @@ class Engine:
         # roctx ranges named by kernel family around the same launches (torch.cuda.nvtx is roctx on ROCm): visible in
         # `rocprofv3 --marker-trace` timelines.  Off by default (a host call per launch).
         self.trace_ranges = False
-        # weight-gradient GEMMs on a side stream (an attribute for A/B runs and tests).  Off by default: measured on
-        # ViT-B/16 B=256 the two streams' GEMMs slow each other down more than the overlap gains (41.3 vs 40.5 ms).
-        self.concurrent_wgrad = False
+        # weight-gradient GEMMs on a side stream (an attribute for A/B runs and tests).  On by default since round 5:
+        # interleaved A/B on one box, ViT-B/16 B=256: 31.53 vs 32.05 ms/step (profiles/r9g_concurrent_wgrad_ab.log;
+        # in round 1, with slower kernels, it had measured 41.3 vs 40.5 ms and was left off)
+        self.concurrent_wgrad = True
         # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend;
         # an attribute, so A/B runs can force either launch mode)
         self.shared_cus = False
