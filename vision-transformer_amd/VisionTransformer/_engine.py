@@ -842,7 +842,14 @@ class Engine:
         mk("ln_bwd", 1)
         outs = [gw[f"{l}.ln1_w"], gw[f"{l}.ln1_b"]] + ([gw[f"{l - 1}.fc2_b"]] if chain_prev else [])
         cs_jobs.append((part, outs, beta))
-        _ops.colsum_finish_batch(cs_jobs)
+        if side is not None:
+            # the partial sums are finished beside the dgrad chain too: only the bucket / optimizer read the results
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            _ops.colsum_finish_batch(cs_jobs, stream=side)
+            for job in cs_jobs:
+                job[0].record_stream(side)
+        else:
+            _ops.colsum_finish_batch(cs_jobs)
         return dx_in, g1n
 
     def run_param_hooks(self):
