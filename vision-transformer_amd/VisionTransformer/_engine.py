@@ -133,6 +133,7 @@ class Engine:
         # interleaved A/B on one box, ViT-B/16 B=256: 31.53 vs 32.05 ms/step (profiles/r9g_concurrent_wgrad_ab.log;
         # in round 1, with slower kernels, it had measured 41.3 vs 40.5 ms and was left off)
         self.concurrent_wgrad = True
+        self.bwd_gemm_tail = None
         # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend;
         # an attribute, so A/B runs can force either launch mode)
         self.shared_cus = False
@@ -615,6 +616,18 @@ class Engine:
         return self._comm_events[0].elapsed_time(self._comm_events[1])
 
     def backward(self, tape, dlogits):
+        """The fused backward (see _backward); `bwd_gemm_tail` (None: the library option as set) switches the split-K
+        tail of the GEMMs for the backward only (the weight-gradient stream fills the partial last rounds there)."""
+        if self.bwd_gemm_tail is None:
+            return self._backward(tape, dlogits)
+        old = _lib.get_option("gemm_tail")
+        _lib.set_option("gemm_tail", int(self.bwd_gemm_tail))
+        try:
+            return self._backward(tape, dlogits)
+        finally:
+            _lib.set_option("gemm_tail", old)
+
+    def _backward(self, tape, dlogits):
         D, T, N, L, dt = self.D, self.T, self.N, self.L, self.dtype
         B = tape.B
         M = B * T
