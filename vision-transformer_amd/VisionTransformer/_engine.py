@@ -661,11 +661,12 @@ class Engine:
         dev = dlogits.device
         dlogits = dlogits.contiguous().float()
         nc = self.nc
+        side = self._side_stream()
         # ---- head (fp32)
         dzn = torch.empty(B, 4 * D, dtype=torch.float32, device=dev)
         self._head_gemm(dlogits, prm["h3_w"], dzn, B, 4 * D, nc, nc, 4 * D, 4 * D, b_kcontig=False)
         if req["h3_w"]:
-            self._wgrad(dlogits, tape.zn, gw["h3_w"], nc, 4 * D, B, nc, 4 * D, beta)
+            self._wgrad(dlogits, tape.zn, gw["h3_w"], nc, 4 * D, B, nc, 4 * D, beta, side)
         if req["h3_b"]:
             self._colsum(dlogits, B, nc, nc, gw["h3_b"], beta)
         dgz = torch.empty_like(tape.gz)
@@ -676,11 +677,13 @@ class Engine:
         dz = torch.empty(B, D, dtype=torch.float32, device=dev)
         self._head_gemm(du, prm["h0_w"], dz, B, D, 4 * D, 4 * D, D, D, b_kcontig=False)
         if req["h0_w"]:
-            self._wgrad(du, tape.z, gw["h0_w"], 4 * D, D, B, 4 * D, D, beta)
+            self._wgrad(du, tape.z, gw["h0_w"], 4 * D, D, B, 4 * D, D, beta, side)
         if req["h0_b"]:
             self._colsum(du, B, 4 * D, 4 * D, gw["h0_b"], beta)
-        self._bucket_ready(self.head_range)
+        self._bucket_ready(self.head_range, side)
         if not need_from[L - 1]:
+            if side is not None:
+                torch.cuda.current_stream(dev).wait_stream(side)      # the head's weight gradients are in G
             self._finish_buckets()
             return None
         # ---- d(encoder output): only token-0 rows are nonzero.  Pruned (see forward): the last block's FFN / proj
@@ -696,7 +699,6 @@ class Engine:
             g1 = _ops.mask4_apply(dx, torch.empty_like(dx), tape.blocks[L - 1][15], 1.0)
         else:
             g1 = dx
-        side = self._side_stream()
         g1_summed = False          # block L-1's fc2 bias gradient: g1 comes from the head (plain column sum below)
         for l in reversed(range(L)):
             if not need_from[l]:
