@@ -1623,7 +1623,8 @@ extern "C" int vit_gemm_split_k_hint(int64_t m, int64_t n, int64_t k, int in_dty
     // may go down to 1 k-tile per slice (option splitk_min_kt overrides the minimum)
     const int64_t min_env = vit::opt(vit::OPT_SPLITK_MIN_KT);
     const int64_t nkt = k / BK, min_kt = min_env > 0 ? min_env : (nkt >= 16 ? 4 : 1);
-    const int64_t s = std::min<int64_t>(std::min<int64_t>(256 / tiles, nkt / min_kt), 64);
+    const int64_t rounds = std::max<int64_t>(1, vit::opt(vit::OPT_SPLITK_ROUNDS));
+    const int64_t s = std::min<int64_t>(std::min<int64_t>(256 * rounds / tiles, nkt / min_kt), 64);
     return (int)std::max<int64_t>(1, s);
   }
   // 128x128 tiles, two per CU, two rounds (also the fp32 parity path's split: its summation order is part of the
