@@ -62,5 +62,42 @@ def main():
         print(f"{name:24s} {timeit(fn):8.3f} ms", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def step_probe():
+    """Whole forward + backward (no optimizer): B=256 vs two B=128 models on two streams at once."""
+    from VisionTransformer.optim import cross_entropy
+    m256, ma, mb = make(256), make(128), make(128)
+    x = torch.randn(256, 3, 224, 224, device="cuda")
+    y = torch.randint(0, 1000, (256,), device="cuda")
+    xa, xb, ya, yb = x[:128].contiguous(), x[128:].contiguous(), y[:128].contiguous(), y[128:].contiguous()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    main_s = torch.cuda.current_stream()
+
+    def fb(m, xx, yy):
+        for p in m.parameters():
+            p.grad = None
+        cross_entropy(m(xx), yy).backward()
+
+    def one():
+        fb(m256, x, y)
+
+    def two():
+        sa.wait_stream(main_s)
+        sb.wait_stream(main_s)
+        with torch.cuda.stream(sa):
+            fb(ma, xa, ya)
+        with torch.cuda.stream(sb):
+            fb(mb, xb, yb)
+        main_s.wait_stream(sa)
+        main_s.wait_stream(sb)
+
+    for name, fn in (("fwd+bwd B=256", one), ("fwd+bwd 2 x B=128 streams", two), ("fwd+bwd B=256", one),
+                     ("fwd+bwd 2 x B=128 streams", two)):
+        print(f"{name:28s} {timeit(fn, 10):8.3f} ms", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "step":
+    step_probe()

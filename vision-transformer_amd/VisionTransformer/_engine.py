@@ -134,6 +134,8 @@ class Engine:
         # in round 1, with slower kernels, it had measured 41.3 vs 40.5 ms and was left off)
         self.concurrent_wgrad = True
         self.bwd_gemm_tail = None
+        self.bwd_priority = False
+        self._hp_stream = None
         # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend;
         # an attribute, so A/B runs can force either launch mode)
         self.shared_cus = False
@@ -618,6 +620,21 @@ class Engine:
     def backward(self, tape, dlogits):
         """The fused backward (see _backward); `bwd_gemm_tail` (None: the library option as set) switches the split-K
         tail of the GEMMs for the backward only (the weight-gradient stream fills the partial last rounds there)."""
+        if self.bwd_priority and self._side_stream() is not None:
+            # the dx chain on a high-priority stream: when both streams have workgroups waiting for a CU, the
+            # dispatcher serves the critical chain first and the weight gradients fill what is left
+            cur = torch.cuda.current_stream(self.device)
+            if self._hp_stream is None or self._hp_stream.device != self.device:
+                lo, hi = torch.cuda.Stream.priority_range()
+                self._hp_stream = torch.cuda.Stream(device=self.device, priority=hi)
+            self._hp_stream.wait_stream(cur)
+            with torch.cuda.stream(self._hp_stream):
+                out = self._backward_tail(tape, dlogits)
+            cur.wait_stream(self._hp_stream)
+            return out
+        return self._backward_tail(tape, dlogits)
+
+    def _backward_tail(self, tape, dlogits):
         if self.bwd_gemm_tail is None:
             return self._backward(tape, dlogits)
         old = _lib.get_option("gemm_tail")
