@@ -133,9 +133,6 @@ class Engine:
         # interleaved A/B on one box, ViT-B/16 B=256: 31.53 vs 32.05 ms/step (profiles/r9g_concurrent_wgrad_ab.log;
         # in round 1, with slower kernels, it had measured 41.3 vs 40.5 ms and was left off)
         self.concurrent_wgrad = True
-        self.bwd_gemm_tail = None
-        self.bwd_priority = False
-        self._hp_stream = None
         # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend;
         # an attribute, so A/B runs can force either launch mode)
         self.shared_cus = False
@@ -618,33 +615,6 @@ class Engine:
         return self._comm_events[0].elapsed_time(self._comm_events[1])
 
     def backward(self, tape, dlogits):
-        """The fused backward (see _backward); `bwd_gemm_tail` (None: the library option as set) switches the split-K
-        tail of the GEMMs for the backward only (the weight-gradient stream fills the partial last rounds there)."""
-        if self.bwd_priority and self._side_stream() is not None:
-            # the dx chain on a high-priority stream: when both streams have workgroups waiting for a CU, the
-            # dispatcher serves the critical chain first and the weight gradients fill what is left
-            cur = torch.cuda.current_stream(self.device)
-            if self._hp_stream is None or self._hp_stream.device != self.device:
-                lo, hi = torch.cuda.Stream.priority_range()
-                self._hp_stream = torch.cuda.Stream(device=self.device, priority=hi)
-            self._hp_stream.wait_stream(cur)
-            with torch.cuda.stream(self._hp_stream):
-                out = self._backward_tail(tape, dlogits)
-            cur.wait_stream(self._hp_stream)
-            return out
-        return self._backward_tail(tape, dlogits)
-
-    def _backward_tail(self, tape, dlogits):
-        if self.bwd_gemm_tail is None:
-            return self._backward(tape, dlogits)
-        old = _lib.get_option("gemm_tail")
-        _lib.set_option("gemm_tail", int(self.bwd_gemm_tail))
-        try:
-            return self._backward(tape, dlogits)
-        finally:
-            _lib.set_option("gemm_tail", old)
-
-    def _backward(self, tape, dlogits):
         D, T, N, L, dt = self.D, self.T, self.N, self.L, self.dtype
         B = tape.B
         M = B * T
