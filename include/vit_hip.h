@@ -50,7 +50,8 @@ const char* vit_last_error(void);
  *   "gemm_impl"          0 automatic (default); 1 / 2 / 4 force the bf16 GEMM kernel generation (register-staged
  *                        128x128 / LDS-DMA 128x128 / LDS-DMA 256x256 ping-pong)
  *   "gemm_tail"          1 (default): split-K tail for a last round of 256x256 tiles that fills at most half the CUs
- *   "gemm_tail_min_kt"   32: minimum k-tiles (K / 64) for that tail
+ *   "gemm_tail_min_kt"   40: minimum k-tiles (K / 64) for that tail (round 5, with the weight gradients on their own
+ *                        stream: the QKV input gradient's tail at K = 2304 (36) measured 0.35 ms/step slower)
  *   "splitk_min_kt"      0 (automatic): minimum k-tiles per K-slice in vit_gemm_split_k_hint
  *   "gemm_group_m"       0 (automatic): tile-row group size of the 256x256 tile order
  *   "gemm_epi_general"   0: 1 forces the general (unspecialised) GEMM epilogue

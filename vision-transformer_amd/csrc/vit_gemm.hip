@@ -1571,6 +1571,8 @@ int tail_split(const vit_gemm_desc* d, int64_t* m_main) {
   // measured (ViT-B/16 B=256, N = 768): a net win at K >= 2304, a loss at K = 768, where a tile's k-loop is short
   // against the slab round trip.  Re-measured with the persistent kernel (tools/bench_ab.sh, whole step): the tail
   // saves 0.45 ms/step; extending it to K = 768 (gemm_tail_min_kt 8: proj, fc1, dgrad fc2 / proj) costs 1.0 ms.
+  // Round 5, with the weight gradients on a second stream filling the idle CUs of a partial round: the QKV input
+  // gradient's tail (K = 2304, 36 k-tiles) costs 0.35 ms/step, the K = 3072 ones (48) still pay: minimum 40.
   const int64_t min_kt = vit::opt(vit::OPT_GEMM_TAIL_MIN_KT);
   if (rounds < 1 || nkt < min_kt) return 1;
   const int64_t mr = rounds * 256 / tn;                    // tile rows that fill whole rounds
