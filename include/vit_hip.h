@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 12
+#define VIT_ABI_VERSION 13
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -117,6 +117,10 @@ typedef struct vit_gemm_desc {
    * (the last block's token-0 rows, ldA = S*K), and its dropout draws the same bits as the full tensor's rows. */
   int64_t dropout_row_stride;
   int32_t flags;      /* VIT_FLAG_* */
+  /* 0, or R0: C's row i is row i + R0 of the tensor its dropout indices refer to ((i + R0) * S * n + j with S the
+   * row stride above): a GEMM over a row range of a larger tensor (one half-batch chain of the forward) draws the
+   * same bits as the whole tensor's rows (ABI 13). */
+  int64_t dropout_row0;
 } vit_gemm_desc;
 
 /* Workspace vit_gemm can use: split_k > 1: the K-split fp32 slabs (required).  split_k <= 1: the slabs of the split-K

@@ -313,6 +313,34 @@ def test_side_stream_weight_gradients_bitwise_equal():
     assert torch.equal(gs[0], gs[1])
 
 
+@pytest.mark.parametrize("dtype,img,train", [(torch.bfloat16, 224, True), (torch.bfloat16, 224, False),
+                                             (torch.float32, 64, True), (torch.bfloat16, 64, True)])
+def test_two_stream_forward_bitwise_equal(dtype, img, train):
+    """The forward's encoder blocks as two half-batch chains on two streams (engine.fwd_streams = 2, the default for
+    batches divisible by 8) equal one chain bit for bit: logits, loss, every gradient (the backward reads the same
+    saved tensors), dropout bits included — the half-batch GEMMs draw the whole batch's dropout indices (vit_gemm_desc
+    dropout_row0).  ViT-B width, 2 blocks (the second pruned, with the query-0 attention), B = 8."""
+    ocfg = O.make_config("micro", img=img, batch=8, blocks=2)
+    ocfg.embedding_size, ocfg.num_heads = 768, 12
+    st = O.init_state(ocfg, seed=8)
+    x, y = O.synthetic_batch(ocfg)
+    out = []
+    for streams in (2, 1):
+        m = _model(ocfg, dtype=dtype)
+        m.load_state_dict(st)
+        m.train(train)
+        m.hip_engine.fwd_streams = streams
+        torch.manual_seed(5)
+        logits = m(x.to(DEV))
+        loss = cross_entropy(logits, y.to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        out.append((logits.detach().clone(), loss.detach().clone(), m.hip_engine.G.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_long_sequence_384_vs_oracle(dtype):
     """BASELINE config 5's sequence length (384^2 / patch 16 -> 576 patches + cls = 577 tokens) at reduced width

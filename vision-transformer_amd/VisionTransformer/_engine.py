@@ -133,6 +133,11 @@ class Engine:
         # interleaved A/B on one box, ViT-B/16 B=256: 31.53 vs 32.05 ms/step (profiles/r9g_concurrent_wgrad_ab.log;
         # in round 1, with slower kernels, it had measured 41.3 vs 40.5 ms and was left off)
         self.concurrent_wgrad = True
+        # the forward's encoder blocks as two half-batch chains on two HIP streams (_forward_blocks_split): each fills
+        # the other's idle CUs (partial last rounds of tiles, kernel drains); outputs bitwise those of one chain
+        self.fwd_streams = 2
+        self._split_fwd = False
+        self._fwd_pair = None
         # backward kernels share the CUs with RCCL collectives (set by enable_data_parallel on the nccl backend;
         # an attribute, so A/B runs can force either launch mode)
         self.shared_cus = False
@@ -364,11 +369,33 @@ class Engine:
 
     def _gemm_rows(self, pr, a, b, c, m, n, k, lda, ldb, ldc, **kw):
         """A token-row GEMM; `pr` (the pruned last block, m = B rows): split-K over the otherwise idle CUs — a few
-        256x256 tiles would each run one long k-loop on one CU."""
+        256x256 tiles would each run one long k-loop on one CU.  (Two-stream forward: each call gets its own slabs,
+        allocated on its stream, instead of the shared workspace.)"""
         split = split_k_for(m, n, k, a.dtype) if pr else 1
         if split > 1:
-            kw.update(split_k=split, workspace=self._workspace(split * m * n * 4))
+            kw.update(split_k=split, workspace=None if self._split_fwd else self._workspace(split * m * n * 4))
         return _ops.gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw)
+
+    @staticmethod
+    def _rows_of(bufs, b0, B, T):
+        """rows(name, token0): this call's slice (images b0 .. b0+B-1) of the whole-batch buffer bufs[name] — T rows
+        per image, or one (token0: the pruned block's token-0 rows); lse by image.  None without bufs."""
+        def rows(name, token0=False):
+            if bufs is None:
+                return None
+            t = bufs[name]
+            per = 1 if (token0 or name == "lse") else T
+            return t[b0 * per:(b0 + B) * per]
+        return rows
+
+    @staticmethod
+    def _mask4_out(bufs, name, r0, R, n, dev):
+        """A VIT_MASK4 buffer for rows r0 .. r0+R-1 of an [.., n] tensor: fresh, or that byte range of bufs[name]
+        (4-row groups: r0 and R multiples of 4)."""
+        if bufs is None:
+            return _ops.mask4_empty(R, n, dev)
+        off = (r0 // 4) * ((n + 3) // 4) * 4
+        return bufs[name][off:off + _ops.mask4_bytes(R, n)]
 
     def _gemm_bwd(self, *args, **kw):
         """A backward GEMM that may overlap the bucket all-reduce (launch mode: self.shared_cus)."""
@@ -452,10 +479,15 @@ class Engine:
         # (rows b*T, row stride T*D; dropout bits drawn at the full tensor's indices) — the same logits, loss and
         # gradients as computing all B*T rows and discarding the rest.  `prune_last = False` computes every row.
         prune = self.prune_last
-        for l in range(L):
-            xcur, saved = self.block_forward(l, xcur, B, training, seed, save, want_probs, prune and l == L - 1)
-            if save:
-                blocks.append(saved)
+        Bh = B // 2
+        if (self.fwd_streams == 2 and not want_probs and self.profile_hook is None and B % 8 == 0
+                and (Bh * T) % 4 == 0):
+            xcur = self._forward_blocks_split(xcur, B, training, seed, save, prune, blocks)
+        else:
+            for l in range(L):
+                xcur, saved = self.block_forward(l, xcur, B, training, seed, save, want_probs, prune and l == L - 1)
+                if save:
+                    blocks.append(saved)
         # classifier on token 0 (= first PATCH, vit.py:80): Linear -> GELU(erf) -> LayerNorm(4D) -> Linear, fp32
         z = torch.empty(B, D, dtype=torch.float32, device=x.device)
         _ops.copy2d(xcur, D if prune else T * D, z, D, B, D)
@@ -470,10 +502,67 @@ class Engine:
             tape.seed, tape.training, tape.pruned = seed, training, prune
         return logits, tape
 
-    def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False):
+    def _block_bufs(self, B, pr, training, save, dev):
+        """Whole-batch outputs of one block for the two-stream forward (the tensors block_forward would allocate)."""
+        D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
+        M = B * T
+        R = B if pr else M
+        e = lambda *shape, dtype=dt: torch.empty(*shape, dtype=dtype, device=dev)   # noqa: E731
+        b = {"a1": e(M, D), "m1": e(M, dtype=torch.float32), "r1": e(M, dtype=torch.float32), "qkv": e(M, 3 * D),
+             "o": e(M, D), "lse": e(B, H, T, dtype=torch.float32), "x_mid": e(R, D), "a2": e(R, D),
+             "m2": e(R, dtype=torch.float32), "r2": e(R, dtype=torch.float32), "h": e(R, 4 * D), "x_out": e(R, D)}
+        if save and not (pr and self.row0_attention) and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
+            b["o32"] = e(M, D, dtype=torch.float32)
+        if save and training:
+            b["pm"] = _ops.mask4_empty(R, D, dev)
+            b["fm"] = _ops.mask4_empty(R, D, dev)
+        if save:
+            b["hm"] = _ops.mask4_empty(R, 4 * D, dev)
+        return b
+
+    def _forward_blocks_split(self, xcur, B, training, seed, save, prune, blocks):
+        """The encoder blocks as two chains of B/2 images on two HIP streams, from the current stream's xcur [B*T, D]
+        (the patch embedding) to the last block's output, which the current stream then waits for.  Every kernel is
+        the one-chain forward's on a row range (rows are independent; dropout indices are the whole batch's), so the
+        outputs are bitwise the same; the two chains fill each other's idle CUs.  The blocks' outputs are whole-batch
+        buffers allocated on the current stream and recorded on both chain streams."""
+        D, T, L = self.D, self.T, self.L
+        dev = xcur.device
+        cur = torch.cuda.current_stream(dev)
+        if self._fwd_pair is None or self._fwd_pair[0].device != dev:
+            self._fwd_pair = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
+        sa, sb = self._fwd_pair
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        Bh, Mh = B // 2, (B // 2) * T
+        names = ("a1", "m1", "r1", "qkv", "o", "o32", "lse", "x_mid", "a2", "m2", "r2", "h", "hm", "pm", "fm")
+        self._split_fwd = True
+        try:
+            for l in range(L):
+                pr = prune and l == L - 1
+                bufs = self._block_bufs(B, pr, training, save, dev)
+                for t in list(bufs.values()) + [xcur]:
+                    t.record_stream(sa)
+                    t.record_stream(sb)
+                for st, b0, xs in ((sa, 0, xcur[:Mh]), (sb, Bh, xcur[Mh:])):
+                    with torch.cuda.stream(st):
+                        self.block_forward(l, xs, Bh, training, seed, save, False, pr, bufs=bufs, b0=b0)
+                if save:
+                    blocks.append((xcur,) + tuple(bufs.get(n) for n in names))
+                xcur = bufs["x_out"]
+        finally:
+            self._split_fwd = False
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+        return xcur
+
+    def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False, bufs=None, b0=0):
         """Block l (transformer.py:76-79) on x_in [B*T, D] (compute dtype): x_mid = x_in + drop(MHA(ln1(x_in))),
         x_out = x_mid + drop(FFN(ln2(x_mid))).  `pr`: the post-attention part on the B token-0 rows only (the pruned
-        last block).  Returns (x_out, saved): `saved` is what block_backward needs (None unless `save`)."""
+        last block).  Returns (x_out, saved): `saved` is what block_backward needs (None unless `save`).
+        `bufs` (the two-stream forward, _forward_blocks_split): the block's outputs for the whole batch, preallocated;
+        this call is images b0 .. b0+B-1 of it and writes their rows (dropout bits drawn at the whole batch's
+        indices), saved = None."""
         model = self.model_ref()
         D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
         M = B * T
@@ -486,14 +575,16 @@ class Engine:
         blk = model.transformer_encoder.blocks[l]
         ln_b = 2 * M * D * es + 8 * M
         mk("ln_fwd", 0, 0.0, ln_b)
-        a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS)
+        rows = self._rows_of(bufs, b0, B, T)                  # this call's slice of a whole-batch buffer
+        a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS,
+                                        y=rows("a1"), mean=rows("m1"), rstd=rows("r1"))
         mk("ln_fwd", 1)
         r0 = pr and self.row0_attention and not want_probs      # the pruned block's attention on query 0 alone
         wq = self.ww[f"{l}.qkv_w"]
         if r0:
             # ... which reads Q of the token-0 rows only: K / V of every row (one GEMM into columns D..3D), Q of the
             # B token-0 rows (split-K over the idle CUs); the other Q rows of qkv are never read
-            qkv = torch.empty(M, 3 * D, dtype=dt, device=dev)
+            qkv = rows("qkv") if bufs is not None else torch.empty(M, 3 * D, dtype=dt, device=dev)
             mk("gemm_fwd", 0, 2.0 * M * 2 * D * D, (M * D + 2 * D * D + 2 * M * D) * es)
             _ops.gemm(a1, wq[D:], qkv[:, D:], M, 2 * D, D, D, D, 3 * D)
             mk("gemm_fwd", 1)
@@ -502,7 +593,7 @@ class Engine:
             mk("gemm_fwd", 1)
         else:
             mk("gemm_fwd", 0, 2.0 * M * 3 * D * D, (M * D + 3 * D * D + 3 * M * D) * es)
-            qkv = _ops.linear(a1, wq)                                               # 3H heads' K/Q/V in one GEMM
+            qkv = _ops.linear(a1, wq) if bufs is None else _ops.gemm(a1, wq, rows("qkv"), M, 3 * D, D, D, D, 3 * D)
             mk("gemm_fwd", 1)
         probs = None
         if want_probs:
@@ -513,47 +604,51 @@ class Engine:
             # O(T hd) per (image, head); o rows b*T and lse[:, :, 0] are written
             o32 = None
             mk("attn_fwd", 0, 4.0 * B * H * T * hd, 2 * M * D * es + 2 * B * D * es + 4 * B * H)
-            o, lse = _ops.attn_fwd_row0(qkv, B, T, H, hd, self.scale)
+            o, lse = _ops.attn_fwd_row0(qkv, B, T, H, hd, self.scale, o=rows("o"), lse=rows("lse"))
             mk("attn_fwd", 1)
         else:
             # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta;
             # the fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
-            o32 = (torch.empty(M, D, dtype=torch.float32, device=dev)
+            o32 = (rows("o32") if bufs is not None and "o32" in bufs else torch.empty(M, D, dtype=torch.float32,
+                                                                                       device=dev)
                    if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
             mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                          else 0))
-            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, probs=probs, o32=o32)
+            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, o=rows("o"), lse=rows("lse"), probs=probs, o32=o32)
             mk("attn_fwd", 1)
         blk.multi_head.attention_probs = probs
         blk.multi_head._probs_skipped = probs is None       # a later read warns once (transformer.py)
         # rows of the post-attention part: all M, or (last block, pruned) the B token-0 rows b*T
         R, rs = (B, T) if pr else (M, 1)
-        pm = _ops.mask4_empty(R, D, dev) if keep_masks else None      # proj dropout keep bits
-        fm = _ops.mask4_empty(R, D, dev) if keep_masks else None      # fc2 dropout keep bits
-        x_mid = torch.empty(R, D, dtype=dt, device=dev)
+        r0 = b0 if pr else b0 * T                                     # this call's first row of the whole batch
+        pm = self._mask4_out(bufs, "pm", r0, R, D, dev) if keep_masks else None      # proj dropout keep bits
+        fm = self._mask4_out(bufs, "fm", r0, R, D, dev) if keep_masks else None      # fc2 dropout keep bits
+        x_mid = rows("x_mid", pr) if bufs is not None else torch.empty(R, D, dtype=dt, device=dev)
         mk("gemm_fwd", 0, 2.0 * R * D * D, (3 * R * D + D * D) * es)
         self._gemm_rows(pr, o, self.ww[f"{l}.proj_w"], x_mid, R, D, D, rs * D, D, D, bias=prm[f"{l}.proj_b"],
                         res=x_in, ldres=rs * D, dropout_p=drop_p, seed=site_seed(seed, l, 0),
-                        drop_row_stride=rs, mask_out=pm)
+                        drop_row_stride=rs, mask_out=pm, drop_row0=r0)
         mk("gemm_fwd", 1)
         mk("ln_fwd", 0, 0.0, 2 * R * D * es + 8 * R)
-        a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS)
+        a2, m2, r2 = _ops.layernorm_fwd(x_mid, prm[f"{l}.ln2_w"], prm[f"{l}.ln2_b"], eps=LN_EPS,
+                                        y=rows("a2", pr), mean=rows("m2", pr), rstd=rows("r2", pr))
         mk("ln_fwd", 1)
         # saved for the backward: the ReLU mask as 1 bit per element (mask4, read by fc2's dgrad epilogue instead
         # of re-reading h: 1/16 of the bytes)
-        hm = _ops.mask4_empty(R, 4 * D, dev) if save else None
+        hm = self._mask4_out(bufs, "hm", r0, R, 4 * D, dev) if save else None
         mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (R * D + 4 * D * D + 4 * R * D) * es + (R * D // 2 if save else 0))
-        h = torch.empty(R, 4 * D, dtype=dt, device=dev)
+        h = rows("h", pr) if bufs is not None else torch.empty(R, 4 * D, dtype=dt, device=dev)
         self._gemm_rows(pr, a2, self.ww[f"{l}.fc1_w"], h, R, 4 * D, D, D, D, 4 * D, bias=prm[f"{l}.fc1_b"],
                         act=ACT_RELU, mask_out=hm)
         mk("gemm_fwd", 1)
-        x_out = torch.empty(R, D, dtype=dt, device=dev)
+        x_out = rows("x_out", pr) if bufs is not None else torch.empty(R, D, dtype=dt, device=dev)
         mk("gemm_fwd", 0, 2.0 * R * 4 * D * D, (4 * R * D + 4 * D * D + 2 * R * D) * es)
         self._gemm_rows(pr, h, self.ww[f"{l}.fc2_w"], x_out, R, D, 4 * D, 4 * D, 4 * D, D, bias=prm[f"{l}.fc2_b"],
                         res=x_mid, ldres=D, dropout_p=drop_p, seed=site_seed(seed, l, 1), drop_row_stride=rs,
-                        mask_out=fm)
+                        mask_out=fm, drop_row0=r0)
         mk("gemm_fwd", 1)
-        saved = (x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm) if save else None
+        saved = (x_in, a1, m1, r1, qkv, o, o32, lse, x_mid, a2, m2, r2, h, hm, pm, fm) if save and bufs is None \
+            else None
         return x_out, saved
 
     # ------------------------------------------------------------------------------------------------------------

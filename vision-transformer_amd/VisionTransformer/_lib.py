@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 F32, BF16, MASK4 = 0, 1, 2
 FLAG_SHARED_CUS = 1          # VIT_FLAG_SHARED_CUS (vit_hip.h)
@@ -38,6 +38,7 @@ class GemmDesc(ctypes.Structure):
         ("mask_out", ctypes.c_void_p),
         ("dropout_row_stride", ctypes.c_int64),
         ("flags", ctypes.c_int32),
+        ("dropout_row0", ctypes.c_int64),
     ]
 
 

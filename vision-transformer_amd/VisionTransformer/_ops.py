@@ -45,13 +45,14 @@ def mask4_empty(m, n, device):
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=1.0, beta=0.0, bias=None,
          act=ACT_NONE, aux=None, ldaux=0, res=None, ldres=0, res_rowmod=0, dropout_p=0.0, seed=0, split_k=1,
          out_group=(0, 0), workspace=None, colsum_part=None, mask_out=None, drop_row_stride=1, shared_cus=False,
-         stream=None):
+         drop_row0=0, stream=None):
     """C[i][j] = epi(alpha * sum_r A(i,r) B(j,r)); see include/vit_hip.h.  `shared_cus`: VIT_FLAG_SHARED_CUS (other
     kernels — RCCL collectives — may hold CUs meanwhile: no persistent grid).  `colsum_part` (f32, colsum_part_rows(m) x n)
     receives per-256-row-block column sums of C as stored — finish with colsum_finish.  `aux` may be a uint8 mask4
     tensor (the ReLU mask saved by the forward); `mask_out` (uint8, mask4_bytes(m, n)) receives C's mask4 (dropout
     keep bits when dropout_p > 0, else C > 0).  `drop_row_stride` S: output row i draws the dropout bits of row i*S of
-    the full tensor (C = token-0 rows of it).  Returns c."""
+    the full tensor (C = token-0 rows of it); `drop_row0` R0: row i draws those of row i + R0 (C = a row range of a
+    larger tensor).  Returns c."""
     _need_cuda(a, b, c, bias, aux, res, colsum_part, mask_out)
     if a.dtype != b.dtype:
         raise TypeError("gemm: A and B dtypes differ")
@@ -79,6 +80,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, a_kcontig=True, b_kcontig=True, alpha=
         d.mask_out = mask_out.data_ptr()
     d.dropout_row_stride = drop_row_stride
     d.flags = FLAG_SHARED_CUS if shared_cus else 0
+    d.dropout_row0 = drop_row0
     if res is not None:
         d.res, d.ldres, d.res_rowmod, d.res_dtype = res.data_ptr(), ldres, res_rowmod, dtype_code(res)
     d.dropout_p, d.dropout_seed = dropout_p, seed & 0xFFFFFFFF
@@ -134,12 +136,12 @@ def embed_cls(cls, pos, x0, B, T, D, stream=None):
     _lib.call("vit_embed_cls", _ptr(cls), _ptr(pos), _ptr(x0), dtype_code(x0), B, T, D, _stream(stream))
 
 
-def layernorm_fwd(x2d, gamma, beta, y=None, eps=1e-5, stream=None):
+def layernorm_fwd(x2d, gamma, beta, y=None, eps=1e-5, stream=None, mean=None, rstd=None):
     _need_cuda(x2d, gamma, beta)
     rows, cols = x2d.shape
     y = torch.empty_like(x2d) if y is None else y
-    mean = torch.empty(rows, dtype=torch.float32, device=x2d.device)
-    rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x2d.device) if mean is None else mean
+    rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device) if rstd is None else rstd
     _lib.call("vit_layernorm_fwd", _ptr(x2d), x2d.stride(0), _ptr(gamma), _ptr(beta), _ptr(y), y.stride(0),
               _ptr(mean), _ptr(rstd), rows, cols, eps, dtype_code(x2d), _stream(stream))
     return y, mean, rstd

@@ -1832,7 +1832,7 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
   if (split_tail || v2_tail) {
     vit_gemm_desc dm = *d;
     dm.m = m_main;
-    const int rc = gemm_run(&dm, 0, stream);
+    const int rc = gemm_run(&dm, d->dropout_row0, stream);
     if (rc) return rc;
     auto esz = [](int32_t t) { return t == VIT_BF16 ? (int64_t)2 : (int64_t)4; };
     const int64_t r = m_main;
@@ -1845,9 +1845,9 @@ extern "C" int vit_gemm(const vit_gemm_desc* d, void* stream) {
     if (d->res) dt.res = (const char*)d->res + r * d->ldres * esz(d->res_dtype);
     if (d->colsum_part) dt.colsum_part = d->colsum_part + (r / 256) * d->n;
     dt.m = d->m - r;
-    if (v2_tail) return gemm_run(&dt, r, stream, 2);
+    if (v2_tail) return gemm_run(&dt, d->dropout_row0 + r, stream, 2);
     dt.split_k = sk;
-    return gemm_run(&dt, r, stream);
+    return gemm_run(&dt, d->dropout_row0 + r, stream);
   }
-  return gemm_run(d, 0, stream);
+  return gemm_run(d, d->dropout_row0, stream);
 }
