@@ -49,9 +49,11 @@ const char* vit_last_error(void);
  * the library has: nothing is read from the environment, so a user's environment cannot change which kernels run.
  *   "gemm_impl"          0 automatic (default); 1 / 2 / 4 force the bf16 GEMM kernel generation (register-staged
  *                        128x128 / LDS-DMA 128x128 / LDS-DMA 256x256 ping-pong)
- *   "gemm_tail"          1 (default): split-K tail for a last round of 256x256 tiles that fills at most half the CUs
- *   "gemm_tail_min_kt"   40: minimum k-tiles (K / 64) for that tail (round 5, with the weight gradients on their own
- *                        stream: the QKV input gradient's tail at K = 2304 (36) measured 0.35 ms/step slower)
+ *   "gemm_tail"          0 (default since round 5): 1 = split-K tail for a last round of 256x256 tiles that fills at
+ *                        most half the CUs.  With the package's two-stream forward and backward the other stream
+ *                        fills those CUs instead: the tails measured 0.18 ms/step slower at C2
+ *   "gemm_tail_min_kt"   40: minimum k-tiles (K / 64) for that tail (with the tail on and the weight gradients on their
+ *                        own stream, the QKV input gradient's tail at K = 2304 (36) measured 0.35 ms/step slower)
  *   "splitk_min_kt"      0 (automatic): minimum k-tiles per K-slice in vit_gemm_split_k_hint
  *   "gemm_group_m"       0 (automatic): tile-row group size of the 256x256 tile order
  *   "gemm_epi_general"   0: 1 forces the general (unspecialised) GEMM epilogue

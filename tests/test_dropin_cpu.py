@@ -227,7 +227,7 @@ def test_engine_roctx_ranges(monkeypatch):
 def test_library_options_host_only():
     """vit_set_option / vit_get_option (vit_hip.h): the documented names and shipped defaults, set/restore, and an
     unknown name refused — host-side only, and the library never reads the environment (no getenv in csrc/)."""
-    defaults = {"gemm_impl": 0, "gemm_tail": 1, "gemm_tail_min_kt": 40, "splitk_min_kt": 0, "gemm_group_m": 0,
+    defaults = {"gemm_impl": 0, "gemm_tail": 0, "gemm_tail_min_kt": 40, "splitk_min_kt": 0, "gemm_group_m": 0,
                 "gemm_epi_general": 0, "gemm_persist": 1, "attn_fwd_split": 0, "attn_bwd_split": 0,
                 "attn_bwd_grid": 0, "ln16": 1, "ln_al": 1, "attn_fwd_ring": 1, "gemm_tail_v2": 0,
                 "splitk_rounds": 1}

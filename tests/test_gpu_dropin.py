@@ -548,7 +548,8 @@ def test_c2_full_shape_bf16_train_vs_oracle():
     two blocks (block 0 runs every GEMM at full M with dense gradients; block 1 is the pruned last block), through the
     engine, against the oracle evaluated on the GPU with torch ops.  This brings the full-size kernels under parity
     test: the K = 50,432 split-K weight-gradient GEMMs, the persistent many-round forward / dgrad GEMMs (591-2,364
-    tiles) and their split-K tails, the 3,072-item persistent attention backward.  Gates of _engine_vs_oracle_on_gpu
+    tiles; their split-K tails are off by default since round 5 and gated at these shapes in test_gpu_kernels), the
+    3,072-item persistent attention backward.  Gates of _engine_vs_oracle_on_gpu
     (logits 1e-2 vs the bf16 oracle, hard)."""
     _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=256, blocks=2, num_classes=1000), seed=23)
 

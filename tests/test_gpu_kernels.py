@@ -308,6 +308,7 @@ def test_gemm_split_k_tail(libopt, variant):
     from VisionTransformer import _lib
     g = torch.Generator().manual_seed(5)
     M, N, K = 90 * 256 + 100, 768, 2304
+    libopt("gemm_tail", 1)                          # off by default since round 5 (the two-stream schedule)
     libopt("gemm_tail_min_kt", 32)                  # K = 2304 (36 k-tiles) is below the shipped minimum (40)
     d = _lib.GemmDesc()
     d.m, d.n, d.k, d.a_kcontig, d.b_kcontig, d.in_dtype, d.out_dtype = M, N, K, 1, 1, 1, 1
@@ -477,6 +478,7 @@ def test_gemm_c2_shapes_tail_split(libopt, shape):
     outputs to bf16 rounding of a different fp32 summation order, identical keep / ReLU bits where the pre-rounding
     values agree, bitwise run to run, and within bf16 tolerance of an fp32 torch product."""
     M, D = 256 * 197, 768
+    libopt("gemm_tail", 1)                          # off by default since round 5 (the two-stream schedule)
     libopt("gemm_tail_min_kt", 32)                  # the QKV input gradient's tail too (K = 2304: 36 k-tiles)
     m, n, k, bkc, kind = {"proj_fwd": (M, D, D, True, "bdr"), "fc2_fwd": (M, D, 4 * D, True, "bdr"),
                           "dgrad_qkv": (M, D, 3 * D, False, "plain"), "fc1_fwd": (M, 4 * D, D, True, "relu_mask"),
