@@ -479,10 +479,10 @@ class Engine:
         # (rows b*T, row stride T*D; dropout bits drawn at the full tensor's indices) — the same logits, loss and
         # gradients as computing all B*T rows and discarding the rest.  `prune_last = False` computes every row.
         prune = self.prune_last
-        Bh = B // 2
-        if (self.fwd_streams == 2 and not want_probs and self.profile_hook is None and B % 8 == 0
-                and (Bh * T) % 4 == 0):
-            xcur = self._forward_blocks_split(xcur, B, training, seed, save, prune, blocks)
+        nc = self.fwd_streams
+        if (nc > 1 and not want_probs and self.profile_hook is None and B % (4 * nc) == 0
+                and ((B // nc) * T) % 4 == 0):
+            xcur = self._forward_blocks_split(xcur, B, training, seed, save, prune, blocks, nc)
         else:
             for l in range(L):
                 xcur, saved = self.block_forward(l, xcur, B, training, seed, save, want_probs, prune and l == L - 1)
@@ -520,8 +520,8 @@ class Engine:
             b["hm"] = _ops.mask4_empty(R, 4 * D, dev)
         return b
 
-    def _forward_blocks_split(self, xcur, B, training, seed, save, prune, blocks):
-        """The encoder blocks as two chains of B/2 images on two HIP streams, from the current stream's xcur [B*T, D]
+    def _forward_blocks_split(self, xcur, B, training, seed, save, prune, blocks, nc=2):
+        """The encoder blocks as nc chains of B/nc images on nc HIP streams (default two), from the current stream's xcur [B*T, D]
         (the patch embedding) to the last block's output, which the current stream then waits for.  Every kernel is
         the one-chain forward's on a row range (rows are independent; dropout indices are the whole batch's), so the
         outputs are bitwise the same; the two chains fill each other's idle CUs.  The blocks' outputs are whole-batch
@@ -529,12 +529,12 @@ class Engine:
         D, T, L = self.D, self.T, self.L
         dev = xcur.device
         cur = torch.cuda.current_stream(dev)
-        if self._fwd_pair is None or self._fwd_pair[0].device != dev:
-            self._fwd_pair = (torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev))
-        sa, sb = self._fwd_pair
-        sa.wait_stream(cur)
-        sb.wait_stream(cur)
-        Bh, Mh = B // 2, (B // 2) * T
+        if self._fwd_pair is None or len(self._fwd_pair) != nc or self._fwd_pair[0].device != dev:
+            self._fwd_pair = tuple(torch.cuda.Stream(device=dev) for _ in range(nc))
+        streams = self._fwd_pair
+        for st in streams:
+            st.wait_stream(cur)
+        Bh, Mh = B // nc, (B // nc) * T
         names = ("a1", "m1", "r1", "qkv", "o", "o32", "lse", "x_mid", "a2", "m2", "r2", "h", "hm", "pm", "fm")
         self._split_fwd = True
         try:
@@ -542,18 +542,19 @@ class Engine:
                 pr = prune and l == L - 1
                 bufs = self._block_bufs(B, pr, training, save, dev)
                 for t in list(bufs.values()) + [xcur]:
-                    t.record_stream(sa)
-                    t.record_stream(sb)
-                for st, b0, xs in ((sa, 0, xcur[:Mh]), (sb, Bh, xcur[Mh:])):
+                    for st in streams:
+                        t.record_stream(st)
+                for i, st in enumerate(streams):
                     with torch.cuda.stream(st):
-                        self.block_forward(l, xs, Bh, training, seed, save, False, pr, bufs=bufs, b0=b0)
+                        self.block_forward(l, xcur[i * Mh:(i + 1) * Mh], Bh, training, seed, save, False, pr,
+                                           bufs=bufs, b0=i * Bh)
                 if save:
                     blocks.append((xcur,) + tuple(bufs.get(n) for n in names))
                 xcur = bufs["x_out"]
         finally:
             self._split_fwd = False
-        cur.wait_stream(sa)
-        cur.wait_stream(sb)
+        for st in streams:
+            cur.wait_stream(st)
         return xcur
 
     def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False, bufs=None, b0=0):
