@@ -537,9 +537,12 @@ class Engine:
         Bh, Mh = B // nc, (B // nc) * T
         names = ("a1", "m1", "r1", "qkv", "o", "o32", "lse", "x_mid", "a2", "m2", "r2", "h", "hm", "pm", "fm")
         self._split_fwd = True
+        # the pruned last block runs whole-batch after the join: split, its B token-0 rows would become two GEMMs of
+        # B/2 rows (below the 256-row tile: the slow small-M kernels)
+        nsplit = L - 1 if prune else L
         try:
-            for l in range(L):
-                pr = prune and l == L - 1
+            for l in range(nsplit):
+                pr = False
                 bufs = self._block_bufs(B, pr, training, save, dev)
                 for t in list(bufs.values()) + [xcur]:
                     for st in streams:
@@ -555,6 +558,10 @@ class Engine:
             self._split_fwd = False
         for st in streams:
             cur.wait_stream(st)
+        if nsplit < L:
+            xcur, saved = self.block_forward(L - 1, xcur, B, training, seed, save, False, True)
+            if save:
+                blocks.append(saved)
         return xcur
 
     def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False, bufs=None, b0=0):
