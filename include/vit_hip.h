@@ -68,6 +68,7 @@ const char* vit_last_error(void);
  *                        tail does not take as 128x128 tiles (two workgroups per CU) in a second launch (measured
  *                        slower at C2: 33.0 vs 31.6 ms/step)
  *   "splitk_rounds"      1: rounds of 256 workgroups the weight-gradient K split aims at (vit_gemm_split_k_hint)
+ *   "attn_fwd_grid"      0 (automatic: one workgroup per CU): workgroups of the persistent ring attention forward
  * vit_set_option returns VIT_ERR_INVALID for an unknown name; vit_get_option returns INT64_MIN for one. */
 int vit_set_option(const char* name, int64_t value);
 int64_t vit_get_option(const char* name);

@@ -230,7 +230,7 @@ def test_library_options_host_only():
     defaults = {"gemm_impl": 0, "gemm_tail": 0, "gemm_tail_min_kt": 40, "splitk_min_kt": 0, "gemm_group_m": 0,
                 "gemm_epi_general": 0, "gemm_persist": 1, "attn_fwd_split": 0, "attn_bwd_split": 0,
                 "attn_bwd_grid": 0, "ln16": 1, "ln_al": 1, "attn_fwd_ring": 1, "gemm_tail_v2": 0,
-                "splitk_rounds": 1}
+                "splitk_rounds": 1, "attn_fwd_grid": 0}
     for k, v in defaults.items():
         assert _lib.get_option(k) == v, k
     with _lib.option("gemm_persist", 0):

@@ -1884,7 +1884,8 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
     if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING)) {
       const int64_t items = B * H;
-      const unsigned grid = (unsigned)std::min<int64_t>(items, vit_cu_count());
+      unsigned grid = (unsigned)std::min<int64_t>(items, vit_cu_count());
+      if (const int64_t gopt = vit::opt(vit::OPT_ATTN_FWD_GRID)) grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, gopt));
 #define RING(NT) \
   attn_fwd_ring<NT><<<grid, NT * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, items, scale)
       switch ((int)((T + 15) / 16)) {
