@@ -502,22 +502,23 @@ class Engine:
             tape.seed, tape.training, tape.pruned = seed, training, prune
         return logits, tape
 
-    def _block_bufs(self, B, pr, training, save, dev):
-        """Whole-batch outputs of one block for the two-stream forward (the tensors block_forward would allocate)."""
+    def _block_bufs(self, B, training, save, dev):
+        """Whole-batch outputs of one (unpruned) block for the two-stream forward: the tensors block_forward would
+        allocate."""
         D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
         M = B * T
-        R = B if pr else M
         e = lambda *shape, dtype=dt: torch.empty(*shape, dtype=dtype, device=dev)   # noqa: E731
-        b = {"a1": e(M, D), "m1": e(M, dtype=torch.float32), "r1": e(M, dtype=torch.float32), "qkv": e(M, 3 * D),
-             "o": e(M, D), "lse": e(B, H, T, dtype=torch.float32), "x_mid": e(R, D), "a2": e(R, D),
-             "m2": e(R, dtype=torch.float32), "r2": e(R, dtype=torch.float32), "h": e(R, 4 * D), "x_out": e(R, D)}
-        if save and not (pr and self.row0_attention) and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
-            b["o32"] = e(M, D, dtype=torch.float32)
+        f32 = torch.float32
+        b = {"a1": e(M, D), "m1": e(M, dtype=f32), "r1": e(M, dtype=f32), "qkv": e(M, 3 * D), "o": e(M, D),
+             "lse": e(B, H, T, dtype=f32), "x_mid": e(M, D), "a2": e(M, D), "m2": e(M, dtype=f32),
+             "r2": e(M, dtype=f32), "h": e(M, 4 * D), "x_out": e(M, D)}
+        if save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
+            b["o32"] = e(M, D, dtype=f32)
         if save and training:
-            b["pm"] = _ops.mask4_empty(R, D, dev)
-            b["fm"] = _ops.mask4_empty(R, D, dev)
+            b["pm"] = _ops.mask4_empty(M, D, dev)
+            b["fm"] = _ops.mask4_empty(M, D, dev)
         if save:
-            b["hm"] = _ops.mask4_empty(R, 4 * D, dev)
+            b["hm"] = _ops.mask4_empty(M, 4 * D, dev)
         return b
 
     def _forward_blocks_split(self, xcur, B, training, seed, save, prune, blocks, nc=2):
@@ -548,14 +549,13 @@ class Engine:
         nsplit = L - 1 if prune else L
         try:
             for l in range(nsplit):
-                pr = False
-                bufs = self._block_bufs(B, pr, training, save, dev)
+                bufs = self._block_bufs(B, training, save, dev)
                 for t in list(bufs.values()) + [xcur]:
                     for st in streams:
                         t.record_stream(st)
                 for i, st in enumerate(streams):
                     with torch.cuda.stream(st):
-                        self.block_forward(l, xcur[i * Mh:(i + 1) * Mh], Bh, training, seed, save, False, pr,
+                        self.block_forward(l, xcur[i * Mh:(i + 1) * Mh], Bh, training, seed, save, False, False,
                                            bufs=bufs, b0=i * Bh)
                 if save:
                     blocks.append((xcur,) + tuple(bufs.get(n) for n in names))
@@ -594,9 +594,9 @@ class Engine:
         a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS,
                                         y=rows("a1"), mean=rows("m1"), rstd=rows("r1"))
         mk("ln_fwd", 1)
-        r0 = pr and self.row0_attention and not want_probs      # the pruned block's attention on query 0 alone
+        q0only = pr and self.row0_attention and not want_probs  # the pruned block's attention on query 0 alone
         wq = self.ww[f"{l}.qkv_w"]
-        if r0:
+        if q0only:
             # ... which reads Q of the token-0 rows only: K / V of every row (one GEMM into columns D..3D), Q of the
             # B token-0 rows (split-K over the idle CUs); the other Q rows of qkv are never read
             qkv = rows("qkv") if bufs is not None else torch.empty(M, 3 * D, dtype=dt, device=dev)
@@ -613,7 +613,7 @@ class Engine:
         probs = None
         if want_probs:
             probs = torch.empty(B, H, T, T, dtype=torch.float32, device=dev)
-        if r0:
+        if q0only:
             # the pruned last block: only attention output row 0 of every image is read (the classifier reads token 0,
             # everything after the attention is per token), and every softmax row is independent -> query 0 alone,
             # O(T hd) per (image, head); o rows b*T and lse[:, :, 0] are written
@@ -624,9 +624,9 @@ class Engine:
         else:
             # training forward in bf16 with the tiled (T > 256) backward: also keep O unrounded for its exact delta;
             # the fused T <= 256 backward forms delta from P and dP itself (vit_hip.h)
-            o32 = (rows("o32") if bufs is not None and "o32" in bufs else torch.empty(M, D, dtype=torch.float32,
-                                                                                       device=dev)
-                   if (save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt)) else None)
+            o32 = None
+            if save and _ops.attn_bwd_uses_o32(B, T, H, hd, dt):
+                o32 = rows("o32") if bufs is not None else torch.empty(M, D, dtype=torch.float32, device=dev)
             mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                          else 0))
             o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, o=rows("o"), lse=rows("lse"), probs=probs, o32=o32)
