@@ -341,6 +341,27 @@ def test_two_stream_forward_bitwise_equal(dtype, img, train):
     assert torch.equal(out[0][2], out[1][2])
 
 
+def test_two_stream_forward_no_grad_bitwise_equal():
+    """The inference forward (torch.no_grad: nothing saved, no masks kept) through the two-chain forward equals one
+    chain bit for bit, in eval and in train mode (dropout drawn, keep bits not stored)."""
+    ocfg = O.make_config("micro", img=224, batch=8, blocks=2)
+    ocfg.embedding_size, ocfg.num_heads = 768, 12
+    st = O.init_state(ocfg, seed=10)
+    x, _ = O.synthetic_batch(ocfg)
+    for train in (False, True):
+        out = []
+        for streams in (2, 1):
+            m = _model(ocfg, dtype=torch.bfloat16)
+            m.load_state_dict(st)
+            m.train(train)
+            m.hip_engine.fwd_streams = streams
+            torch.manual_seed(3)
+            with torch.no_grad():
+                out.append(m(x.to(DEV)).clone())
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], out[1]), train
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_long_sequence_384_vs_oracle(dtype):
     """BASELINE config 5's sequence length (384^2 / patch 16 -> 576 patches + cls = 577 tokens) at reduced width
