@@ -466,13 +466,6 @@ class Engine:
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training else 0
         tape = Tape() if save else None
 
-        cols = _ops.im2col(x, self.P, dt)                                             # vit.py:21-29 as GEMM
-        xcur = torch.empty(M, D, dtype=dt, device=x.device)
-        mk("gemm_fwd", 0, 2.0 * B * N * D * self.CPP, (B * N + D) * self.CPP * es + B * N * D * es)
-        _ops.gemm(cols, self.ww["conv_w"], xcur, B * N, D, self.CPP, self.CPP, self.CPP, D, bias=prm["conv_b"],
-                  res=prm["pos"].view(T, D), ldres=D, res_rowmod=N, out_group=(N, T))  # + pos, rows -> b*T+n
-        mk("gemm_fwd", 1)
-        _ops.embed_cls(prm["cls"], prm["pos"], xcur, B, T, D)                           # CLS appended LAST (vit.py:41)
         blocks = []
         # The classifier reads token 0 of the last block's output only (vit.py:80), and everything after the last
         # attention is per token: the last block's proj / LN2 / MLP (and their backward) run on the B token-0 rows
@@ -480,10 +473,13 @@ class Engine:
         # gradients as computing all B*T rows and discarding the rest.  `prune_last = False` computes every row.
         prune = self.prune_last
         nc = self.fwd_streams
+        cols = torch.empty(B * N, self.CPP, dtype=dt, device=x.device)
+        xcur = torch.empty(M, D, dtype=dt, device=x.device)
         if (nc > 1 and not want_probs and self.profile_hook is None and B % (4 * nc) == 0
                 and ((B // nc) * T) % 4 == 0):
-            xcur = self._forward_blocks_split(xcur, B, training, seed, save, prune, blocks, nc)
+            xcur = self._forward_blocks_split(x, cols, xcur, B, training, seed, save, prune, blocks, nc)
         else:
+            self._embed(x, cols, xcur, 0, B)
             for l in range(L):
                 xcur, saved = self.block_forward(l, xcur, B, training, seed, save, want_probs, prune and l == L - 1)
                 if save:
@@ -521,12 +517,29 @@ class Engine:
             b["hm"] = _ops.mask4_empty(M, 4 * D, dev)
         return b
 
-    def _forward_blocks_split(self, xcur, B, training, seed, save, prune, blocks, nc=2):
-        """The encoder blocks as nc chains of B/nc images on nc HIP streams (default two), from the current stream's xcur [B*T, D]
-        (the patch embedding) to the last block's output, which the current stream then waits for.  Every kernel is
-        the one-chain forward's on a row range (rows are independent; dropout indices are the whole batch's), so the
-        outputs are bitwise the same; the two chains fill each other's idle CUs.  The blocks' outputs are whole-batch
-        buffers allocated on the current stream and recorded on both chain streams."""
+    def _embed(self, x, cols, xcur, b0, B):
+        """Patch embedding (vit.py:21-29, 39-42) of images b0 .. b0+B-1 into their rows of the whole-batch cols /
+        xcur: im2col, the conv as a GEMM with conv bias + pos and the (b, n) -> b*T + n row remap in its epilogue,
+        then the CLS rows (appended LAST, vit.py:41)."""
+        D, T, N, dt = self.D, self.T, self.N, self.dtype
+        es = 2 if dt == torch.bfloat16 else 4
+        prm = self.params
+        cl = cols[b0 * N:(b0 + B) * N]
+        xc = xcur[b0 * T:(b0 + B) * T]
+        _ops.im2col(x[b0:b0 + B], self.P, dt, cols=cl)                                # vit.py:21-29 as GEMM
+        self._mark("gemm_fwd", 0, 2.0 * B * N * D * self.CPP, (B * N + D) * self.CPP * es + B * N * D * es)
+        _ops.gemm(cl, self.ww["conv_w"], xc, B * N, D, self.CPP, self.CPP, self.CPP, D, bias=prm["conv_b"],
+                  res=prm["pos"].view(T, D), ldres=D, res_rowmod=N, out_group=(N, T))  # + pos, rows -> b*T+n
+        self._mark("gemm_fwd", 1)
+        _ops.embed_cls(prm["cls"].reshape(-1, D)[b0:b0 + B], prm["pos"], xc, B, T, D)  # CLS appended LAST
+
+    def _forward_blocks_split(self, x, cols, xcur, B, training, seed, save, prune, blocks, nc=2):
+        """The patch embedding and the encoder blocks as nc chains of B/nc images on nc HIP streams (default two),
+        into the whole-batch cols / xcur allocated on the current stream, up to the last block's output, which the
+        current stream then waits for.  Every kernel is the one-chain forward's on a row range (rows are
+        independent; dropout indices are the whole batch's), so the outputs are bitwise the same; the chains fill
+        each other's idle CUs.  The blocks' outputs are whole-batch buffers allocated on the current stream and
+        recorded on every chain stream."""
         D, T, L = self.D, self.T, self.L
         dev = xcur.device
         cur = torch.cuda.current_stream(dev)
@@ -536,6 +549,12 @@ class Engine:
         for st in streams:
             st.wait_stream(cur)
         Bh, Mh = B // nc, (B // nc) * T
+        for t in (x, cols, xcur):
+            for st in streams:
+                t.record_stream(st)
+        for i, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                self._embed(x, cols, xcur, i * Bh, Bh)
         names = ("a1", "m1", "r1", "qkv", "o", "o32", "lse", "x_mid", "a2", "m2", "r2", "h", "hm", "pm", "fm")
         # the ring attention forward of one chain on 3/4 of the CUs, so the other chain's GEMMs run beside it instead
         # of waiting for the whole latency-bound kernel (one box, interleaved: 30.50 -> 30.19 ms/step; 1/2 and 7/8 of

@@ -115,11 +115,11 @@ def linear(x2d, w, bias=None, out_dtype=None, act=ACT_NONE, **kw):
     return gemm(x2d, w, y, M, N, K, x2d.stride(0), w.stride(0), N, bias=bias, act=act, **kw)
 
 
-def im2col(x, P, dtype, stream=None):
+def im2col(x, P, dtype, stream=None, cols=None):
     _need_cuda(x)
     B, C, H, W = x.shape
     n = (H // P) * (W // P)
-    cols = torch.empty(B * n, C * P * P, dtype=dtype, device=x.device)
+    cols = torch.empty(B * n, C * P * P, dtype=dtype, device=x.device) if cols is None else cols
     _lib.call("vit_im2col", _ptr(x), dtype_code(x), _ptr(cols), dtype_code(dtype), B, C, H, W, P, _stream(stream))
     return cols
 
