@@ -582,21 +582,42 @@ class Engine:
         finally:
             self._split_fwd = False
             _lib.set_option("attn_fwd_grid", grid_opt)
+        pre = None
+        if nsplit < L and self.row0_attention:
+            # the pruned block's ln1 and K / V GEMM are whole-row work: per chain too
+            l = L - 1
+            D = self.D
+            pre = (torch.empty(B * T, D, dtype=self.dtype, device=dev),
+                   torch.empty(B * T, dtype=torch.float32, device=dev),
+                   torch.empty(B * T, dtype=torch.float32, device=dev),
+                   torch.empty(B * T, 3 * D, dtype=self.dtype, device=dev))
+            for t in pre:
+                for st in streams:
+                    t.record_stream(st)
+            wq = self.ww[f"{l}.qkv_w"]
+            for i, st in enumerate(streams):
+                r = slice(i * Mh, (i + 1) * Mh)
+                with torch.cuda.stream(st):
+                    _ops.layernorm_fwd(xcur[r], self.params[f"{l}.ln1_w"], self.params[f"{l}.ln1_b"], eps=LN_EPS,
+                                       y=pre[0][r], mean=pre[1][r], rstd=pre[2][r])
+                    _ops.gemm(pre[0][r], wq[D:], pre[3][r][:, D:], Mh, 2 * D, D, D, D, 3 * D)
         for st in streams:
             cur.wait_stream(st)
         if nsplit < L:
-            xcur, saved = self.block_forward(L - 1, xcur, B, training, seed, save, False, True)
+            xcur, saved = self.block_forward(L - 1, xcur, B, training, seed, save, False, True, pre=pre)
             if save:
                 blocks.append(saved)
         return xcur
 
-    def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False, bufs=None, b0=0):
+    def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False, bufs=None, b0=0,
+                      pre=None):
         """Block l (transformer.py:76-79) on x_in [B*T, D] (compute dtype): x_mid = x_in + drop(MHA(ln1(x_in))),
         x_out = x_mid + drop(FFN(ln2(x_mid))).  `pr`: the post-attention part on the B token-0 rows only (the pruned
         last block).  Returns (x_out, saved): `saved` is what block_backward needs (None unless `save`).
         `bufs` (the two-stream forward, _forward_blocks_split): the block's outputs for the whole batch, preallocated;
         this call is images b0 .. b0+B-1 of it and writes their rows (dropout bits drawn at the whole batch's
-        indices), saved = None."""
+        indices), saved = None.  `pre` (the pruned block after the two-chain forward): its ln1 output / statistics and
+        qkv with the K / V columns already computed per chain; only the token-0 rows' Q GEMM is left."""
         model = self.model_ref()
         D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
         M = B * T
@@ -610,18 +631,23 @@ class Engine:
         ln_b = 2 * M * D * es + 8 * M
         mk("ln_fwd", 0, 0.0, ln_b)
         rows = self._rows_of(bufs, b0, B, T)                  # this call's slice of a whole-batch buffer
-        a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS,
-                                        y=rows("a1"), mean=rows("m1"), rstd=rows("r1"))
-        mk("ln_fwd", 1)
         q0only = pr and self.row0_attention and not want_probs  # the pruned block's attention on query 0 alone
         wq = self.ww[f"{l}.qkv_w"]
+        if pre is not None:
+            a1, m1, r1, qkv = pre
+            mk("ln_fwd", 1)
+        else:
+            a1, m1, r1 = _ops.layernorm_fwd(x_in, prm[f"{l}.ln1_w"], prm[f"{l}.ln1_b"], eps=LN_EPS,
+                                            y=rows("a1"), mean=rows("m1"), rstd=rows("r1"))
+            mk("ln_fwd", 1)
         if q0only:
             # ... which reads Q of the token-0 rows only: K / V of every row (one GEMM into columns D..3D), Q of the
             # B token-0 rows (split-K over the idle CUs); the other Q rows of qkv are never read
-            qkv = rows("qkv") if bufs is not None else torch.empty(M, 3 * D, dtype=dt, device=dev)
-            mk("gemm_fwd", 0, 2.0 * M * 2 * D * D, (M * D + 2 * D * D + 2 * M * D) * es)
-            _ops.gemm(a1, wq[D:], qkv[:, D:], M, 2 * D, D, D, D, 3 * D)
-            mk("gemm_fwd", 1)
+            if pre is None:
+                qkv = rows("qkv") if bufs is not None else torch.empty(M, 3 * D, dtype=dt, device=dev)
+                mk("gemm_fwd", 0, 2.0 * M * 2 * D * D, (M * D + 2 * D * D + 2 * M * D) * es)
+                _ops.gemm(a1, wq[D:], qkv[:, D:], M, 2 * D, D, D, D, 3 * D)
+                mk("gemm_fwd", 1)
             mk("gemm_fwd", 0, 2.0 * B * D * D, (2 * B * D + D * D) * es)
             self._gemm_rows(True, a1, wq, qkv, B, D, D, T * D, D, T * 3 * D)
             mk("gemm_fwd", 1)
