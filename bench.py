@@ -82,6 +82,15 @@ def pmc_traffic(key, family):
         return None, None
 
 
+def pmc_schedule(key):
+    """The schedule the PMC passes of profiles/pmc_<key>.json ran (tools/gpu_profile.sh), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{key}.json")) as f:
+            return json.load(f).get("schedule", "default (two forward chains + weight-gradient stream)")
+    except (OSError, ValueError):
+        return None
+
+
 def gemm_peak(dev, n=8192, reps=5):
     """Measured dense bf16 MFMA GEMM rate on this device: this library's GEMM and hipBLASLt
     (torch.matmul) on one n^3 GEMM of uniform [-1, 1) operands, outside the timed steps."""
@@ -413,6 +422,7 @@ def run(args, rank, world, local):
                     "algorithmic_bytes_per_launch": int(d["bytes_per_step"] / d["launches_per_step"]),
                     "algorithmic_bytes_per_step": int(d["bytes_per_step"]),
                     "pmc_mfma_busy_frac": pmc.get("mfma_busy_frac") if pmc else None,
+                    "pmc_schedule": pmc_schedule(key),
                     "traffic_source": f"profiles/pmc_{key}.json" if traffic is not None else None,
                     "ms_per_step": d["ms_per_step"], "launches_per_step": d["launches_per_step"],
                     "events_over": "every hot launch of the last of the timed steps (HIP events on the compute stream)",

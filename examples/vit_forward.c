@@ -231,7 +231,7 @@ int main(int argc, char** argv) {
   for (int l = 0; l < z.L; ++l) { /* Block (transformer.py:66-79), pre-LN, eval mode */
     VIT_CHECK(vit_layernorm_fwd(x, D, blk[l].ln1_w, blk[l].ln1_b, a1, D, mean, rstd, T, D, 1e-5f, dt, g_stream));
     linear(a1, blk[l].qkv_w, qkv, T, 3 * D, D, dt, dt, NULL, VIT_ACT_NONE, NULL, 0, 0, 0, 0, 0, 3 * D);
-    VIT_CHECK(vit_attn_fwd(qkv, o, NULL, lse, NULL, 1, T, z.H, z.hd, scale, dt, g_stream));
+    VIT_CHECK(vit_attn_fwd(qkv, o, NULL, lse, NULL, 1, T, z.H, z.hd, scale, dt, 0, g_stream));
     linear(o, blk[l].proj_w, xm, T, D, D, dt, dt, blk[l].proj_b, VIT_ACT_NONE, x, dt, D, 0, 0, 0, D);
     VIT_CHECK(vit_layernorm_fwd(xm, D, blk[l].ln2_w, blk[l].ln2_b, a1, D, mean, rstd, T, D, 1e-5f, dt, g_stream));
     linear(a1, blk[l].fc1_w, hbuf, T, F, D, dt, dt, blk[l].fc1_b, VIT_ACT_RELU, NULL, 0, 0, 0, 0, 0, F);

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define VIT_ABI_VERSION 13
+#define VIT_ABI_VERSION 14
 
 typedef enum { VIT_OK = 0, VIT_ERR_INVALID = 1, VIT_ERR_LAUNCH = 2 } vit_status;
 typedef enum { VIT_F32 = 0, VIT_BF16 = 1, VIT_MASK4 = 2 } vit_dtype;
@@ -69,6 +69,7 @@ const char* vit_last_error(void);
  *                        slower at C2: 33.0 vs 31.6 ms/step)
  *   "splitk_rounds"      1: rounds of 256 workgroups the weight-gradient K split aims at (vit_gemm_split_k_hint)
  *   "attn_fwd_grid"      0 (automatic: one workgroup per CU): workgroups of the persistent ring attention forward
+ *                        when the call's own max_wgs is 0
  * vit_set_option returns VIT_ERR_INVALID for an unknown name; vit_get_option returns INT64_MIN for one. */
 int vit_set_option(const char* name, int64_t value);
 int64_t vit_get_option(const char* name);
@@ -188,10 +189,13 @@ int vit_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, 
  *   - the tiled backward (T > 256) takes delta from o32 when given: the forward then also stores O unrounded,
  *     [B*T][D] f32 (o32 == NULL: the bf16 O, standard flash-attention practice, cheaper but inexact).
  *   vit_attn_bwd_uses_o32() says which one a shape runs (1: pass o32 to the forward and the backward).
+ * fwd max_wgs (ABI 14): 0 = automatic (one workgroup per CU, or option "attn_fwd_grid"); > 0 = the persistent ring
+ *   forward (T <= 256) runs at most max_wgs workgroups — per call, so two callers on two threads or streams never
+ *   share the choice (the package's two-stream forward gives one chain 3/4 of the CUs this way).  Other forms ignore it.
  * bwd: dqkv[B*T][3*D]; workspace = vit_attn_bwd_workspace_bytes.
  * ------------------------------------------------------------------------------------------------------------ */
 int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, float* probs, int64_t B, int64_t T, int64_t H,
-                 int64_t hd, float scale, int32_t dtype, void* stream);
+                 int64_t hd, float scale, int32_t dtype, int64_t max_wgs, void* stream);
 int vit_attn_bwd_uses_o32(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
 int64_t vit_attn_bwd_workspace_bytes(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype);
 int vit_attn_bwd(const void* qkv, const void* o, const float* o32, const void* d_o, const float* lse, void* dqkv,

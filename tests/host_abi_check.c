@@ -74,7 +74,7 @@ int main(void) {
   CHECK(vit_resize_ksize(512, 224) >= 1);
 
   /* entry points that refuse before the device */
-  CHECK(refused(vit_attn_fwd(NULL, NULL, NULL, NULL, NULL, 1, 1, 1, 64, 1.f, VIT_BF16, NULL), "vit_attn_fwd"));
+  CHECK(refused(vit_attn_fwd(NULL, NULL, NULL, NULL, NULL, 1, 1, 1, 64, 1.f, VIT_BF16, 0, NULL), "vit_attn_fwd"));
   CHECK(refused(vit_attn_bwd(NULL, NULL, NULL, NULL, NULL, NULL, 1, 1, 1, 64, 1.f, VIT_BF16, NULL, 0, NULL),
                 "vit_attn_bwd"));
   CHECK(refused(vit_attn_fwd_row0(NULL, NULL, NULL, 1, 1, 1, 64, 1.f, VIT_BF16, NULL), "vit_attn_fwd_row0"));

@@ -431,6 +431,8 @@ def _dp_train_worker(rank, world, port, q):
     with tempfile.TemporaryDirectory() as tmp:
         T.train(cfg, dl, None, 1, 1, os.path.join(tmp, "l"), os.path.join(tmp, "ck"))     # epochs 0 and 1
     orders = [ds.seen[:8], ds.seen[8:16]]
+    # after train() each replica's CPU RNG (the host dropout's) is its own stream: keep masks differ per rank
+    drop = torch.nn.functional.dropout(torch.ones(256), 0.2, True).ne(0).tolist()
     # evaluate(): each rank scores its shard of a test set whose size (37) divides neither by the world size nor by the
     # batch: ShardSampler shards (partial last batches, padded for the model), and DistributedSampler shards (padding
     # duplicates dropped); both must give the accuracy over the 37 unique samples
@@ -461,7 +463,7 @@ def _dp_train_worker(rank, world, port, q):
             pr = torch.cat([vm(xp[i:i + 4]) for i in range(0, len(xp), 4)])[:len(idx)].argmax(-1)
             correct += int((pr == ys).sum())
     v_want = correct / 37
-    q.put((rank, orders, accs, want, v_acc, v_want))
+    q.put((rank, orders, accs, want, v_acc, v_want, drop))
     dist.destroy_process_group()
 
 
@@ -480,7 +482,8 @@ def test_data_parallel_train_epochs_and_evaluate_gloo():
     res = sorted(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    (r0, o0, a0, w0, v0, vw0), (r1, o1, a1, w1, v1, vw1) = res
+    (r0, o0, a0, w0, v0, vw0, d0), (r1, o1, a1, w1, v1, vw1, d1) = res
+    assert d0 != d1                                               # per-replica dropout streams
     for e in range(2):
         assert sorted(o0[e] + o1[e]) == list(range(16)), e       # the shards partition the set every epoch
     assert o0[0] != o0[1] and o1[0] != o1[1]                      # set_epoch: a new order each epoch
@@ -488,6 +491,43 @@ def test_data_parallel_train_epochs_and_evaluate_gloo():
     for a in a0 + a1:
         assert abs(a - w0) < 1e-12, (a0, a1, w0)                  # exact whole-set accuracy over unique samples
     assert abs(v0 - vw0) < 1e-12 and v0 == v1
+
+
+def _dropout_rank_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = vit.VisionTransformer(_cfg("micro")).enable_data_parallel()
+    q.put((rank, m.hip_engine.dropout_rank))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_dropout_differs_per_rank():
+    """Every rank draws the same base dropout seed (identically seeded CPU RNG, needed for identical init), so the
+    engine folds the replica index in: enable_data_parallel sets it to the group rank; rank 0 keeps
+    the single-process seed; the ranks' seeds, and the keep masks they hash to at every site, all differ."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dropout_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == [(0, 0), (1, 1)]
+    for base in (0, 1, 12345, 2 ** 31 - 2):
+        seeds = [_engine.dropout_seed(base, r) for r in range(8)]
+        assert seeds[0] == base and len(set(seeds)) == 8 and all(0 <= s < 2 ** 31 for s in seeds)
+        for layer in (0, 11):
+            for site in (0, 1):
+                masks = [O.dropout_keep(_engine.site_seed(s, layer, site), (197, 64)) for s in seeds]
+                for i in range(8):
+                    assert abs(masks[i].float().mean().item() - 0.8) < 0.02
+                    for j in range(i):
+                        assert not torch.equal(masks[i], masks[j])
 
 
 def test_attention_probs_warns_once_after_fused_forward():

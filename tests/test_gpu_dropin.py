@@ -469,6 +469,33 @@ def test_fused_adamw_follows_repointed_storage():
         assert (p.detach() - r.detach()).abs().max().item() < 1e-6
 
 
+def test_fused_adamw_follows_repointed_grad_storage():
+    """a .grad tensor object that stays the same while its storage is re-pointed (`p.grad.data = t`,
+    `p.grad.set_(t)`) after the chunk table was cached: the next steps read the new gradient storage."""
+    torch.manual_seed(1)
+    ps = [torch.randn(37, 5, device=DEV).requires_grad_(True), torch.randn(300, device=DEV).requires_grad_(True)]
+    ref = [p.detach().clone().requires_grad_(True) for p in ps]
+    for p, r in zip(ps, ref):                   # persistent gradient objects, written in place (the engine's way)
+        p.grad, r.grad = torch.zeros_like(p), torch.zeros_like(r)
+    opt = FusedAdamW(ps, lr=1e-2, weight_decay=1e-2)
+    ropt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=1e-2)
+    for i in range(5):
+        grads = [torch.randn_like(p) for p in ps]
+        for j, (p, g) in enumerate(zip(ps, grads)):
+            if (i, j) == (2, 0):
+                p.grad.data = g.clone()                 # same object, new storage
+            elif (i, j) == (3, 1):
+                p.grad.set_(g.clone())
+            else:
+                p.grad.copy_(g)
+        for r, g in zip(ref, grads):
+            r.grad.copy_(g)
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, ref):
+        assert (p.detach() - r.detach()).abs().max().item() < 1e-6
+
+
 def test_missing_library_fails_loudly(monkeypatch):
     """No silent fallback: a device model with libvit_hip.so absent raises (the host path is never used for device
     tensors)."""
@@ -552,6 +579,17 @@ def test_c2_full_shape_bf16_train_vs_oracle():
     3,072-item persistent attention backward.  Gates of _engine_vs_oracle_on_gpu
     (logits 1e-2 vs the bf16 oracle, hard)."""
     _engine_vs_oracle_on_gpu(O.make_config("base", img=224, batch=256, blocks=2, num_classes=1000), seed=23)
+
+
+def test_vit_large_width_two_chain_ragged_ring_vs_oracle():
+    """C4's ViT-L width (D = 1024, H = 16, T = 197) bf16 train through the default two-chain forward (fwd_streams 2)
+    at B = 32: each chain's ring attention forward runs its 16 x 16 = 256 items on the 3/4-CU grid
+    (192 workgroups: 64 of them take a second item, the rest one), the ragged multi-item case C4 itself hits at
+    B = 128 (1,024 items per chain).  Gates of _engine_vs_oracle_on_gpu (logits 1e-2 vs the bf16 oracle)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    items = (32 // 2) * 16
+    assert items > cus * 3 // 4 and items % (cus * 3 // 4) != 0
+    _engine_vs_oracle_on_gpu(O.make_config("large", img=224, batch=32, blocks=2, num_classes=1000), seed=31)
 
 
 def test_vit_base_full_depth_bf16_train_properties():

@@ -678,6 +678,43 @@ def test_attention_bwd_shared_cus_bitwise(libopt, grid):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("T", [197, 209, 240, 256])
+def test_attention_fwd_ring_ragged_grids(libopt, T):
+    """The persistent ring forward (attn_fwd_ring<NT>) where workgroups take several items and the item count is not a
+    multiple of the grid: B = 17, H = 12 (204 items) over 64 and 192 workgroups (per call, max_wgs)
+    and over the option attn_fwd_grid; T = 197 is the 3-slot ring (NT 13), T = 209 / 240 / 256 the 2-slot ring (NT
+    14-16).  Against fp64 on the same bf16 inputs (o to 2e-2 of the largest value, lse to 1e-3), bitwise equal over
+    every grid (items are independent), and within the same gate of the one-workgroup-per-item forward."""
+    torch.manual_seed(T)
+    B, H, hd = 17, 12, 64
+    D = H * hd
+    qkv = (torch.randn(B * T, 3 * D, device=DEV) * 0.5).bfloat16()
+    x = qkv.double()
+    q, k, v = x.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * 8.0
+    o_ref = (torch.softmax(s, -1) @ v).permute(0, 2, 1, 3).reshape(B * T, D)
+    lse_ref = torch.logsumexp(s, -1)
+    scale_o = max(1.0, float(o_ref.abs().max()))
+    outs = []
+    for wgs, opt in ((64, 0), (192, 0), (0, 0), (0, 50)):
+        libopt("attn_fwd_grid", opt)
+        o = torch.full((B * T, D), 3.0, device=DEV, dtype=torch.bfloat16)
+        lse = torch.full((B, H, T), 3.0, device=DEV)
+        o, lse = _ops.attn_fwd(qkv, B, T, H, hd, 8.0, o=o, lse=lse, max_wgs=wgs)
+        torch.cuda.synchronize()
+        err = float((o.double() - o_ref).abs().max())
+        assert err <= 2e-2 * scale_o, (wgs, opt, err)
+        assert float((lse.double() - lse_ref).abs().max()) <= 1e-3 * max(1.0, float(lse_ref.abs().max())), (wgs, opt)
+        outs.append((o, lse))
+    for o, lse in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(lse, outs[0][1])
+    libopt("attn_fwd_grid", 0)
+    libopt("attn_fwd_ring", 0)
+    of, lf = _ops.attn_fwd(qkv, B, T, H, hd, 8.0)
+    assert float((of.double() - outs[0][0].double()).abs().max()) <= 2e-2 * scale_o
+    assert float((lf - outs[0][1]).abs().max()) <= 1e-3 * max(1.0, float(lse_ref.abs().max()))
+
+
 @pytest.mark.parametrize("T", [1, 31, 32, 33, 197, 256])
 def test_attention_fwd_fused_matches_split(libopt, T):
     """The one-workgroup-per-(image, head) forward (T <= 256) against the 128-query-tile kernel and fp32."""

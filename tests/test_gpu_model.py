@@ -15,7 +15,7 @@ from oracle import vit_oracle as O
 pytestmark = pytest.mark.gpu
 
 if torch.cuda.is_available():
-    from VisionTransformer import _ops, config, transformer, vit
+    from VisionTransformer import _lib, _ops, config, transformer, vit
     from VisionTransformer.optim import FusedAdamW, cross_entropy
 
 DEV = "cuda"
@@ -129,10 +129,12 @@ def test_tiny_c1_fp32_vs_reference(golden_dir):
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     st = O.init_state(ocfg, 0)
     _, _, g_seq = O.loss_and_grads(st, x.cpu(), y.cpu(), ocfg, seq_chain=True)
-    # Each scale is a single sample of chaotic rounding amplification, so the per-tensor gate is 8x, and the whole
-    # gradient vector (all tensors' slices concatenated) must be within 2x of the sequential-order sample.
+    # Each scale is a single sample of chaotic rounding amplification; the per-tensor gate is 4x (round 6: was 8x),
+    # and the whole gradient vector (all tensors' slices concatenated) must be within 2x of the sequential-order
+    # sample.
     params = dict(m.named_parameters())
     cat = {"ours": [], "seq": [], "r64": []}
+    ratios = []
     for k in params:
         ours = params[k].grad.cpu().reshape(-1)[::97].double().numpy()
         r32, r64 = g["gslice/" + k].astype(np.float64), g["gslice64/" + k]
@@ -140,9 +142,11 @@ def test_tiny_c1_fp32_vs_reference(golden_dir):
         n64 = max(np.linalg.norm(r64), 1e-30)
         e_ours = np.linalg.norm(ours - r64) / n64
         e_ref = max(np.linalg.norm(r32 - r64), np.linalg.norm(rsq - r64)) / n64
-        assert e_ours <= max(2e-4, 8 * e_ref), (k, e_ours, e_ref)
+        ratios.append((e_ours / max(e_ref, 1e-12), k))
+        assert e_ours <= max(2e-4, 4 * e_ref), (k, e_ours, e_ref)
         for n_, v_ in (("ours", ours), ("seq", rsq), ("r64", r64)):
             cat[n_].append(v_)
+    print("ViT-Tiny fp32 worst gradient error ratios (ours / valid-order error):", sorted(ratios)[-4:])
     o, sq, r = (np.concatenate(cat[n_]) for n_ in ("ours", "seq", "r64"))
     assert np.linalg.norm(o - r) <= max(1e-5 * np.linalg.norm(r), 2 * np.linalg.norm(sq - r))
     # 3-step AdamW trace: step 1 is the same loss; later steps are AdamW-chaotic (first updates ~ lr*sign(g)),
@@ -293,6 +297,32 @@ def test_pruned_last_block_matches_all_rows(dtype, train):
         assert errs[-1][0] < tol, errs[-1]
 
 
+@pytest.mark.parametrize("first", [True, False], ids=["row0_fwd", "full_fwd"])
+def test_row0_mode_recorded_on_tape(first):
+    """The backward of the pruned block runs the attention backward matching the forward it saved (Tape.row0), even
+    when engine.row0_attention is flipped between the two (the full backward would read o / lse rows the
+    query-0 forward never wrote): bitwise equal to the unflipped run."""
+    ocfg = O.make_config("micro", img=64, batch=8, blocks=2)
+    ocfg.embedding_size, ocfg.num_heads = 256, 4
+    st = O.init_state(ocfg, seed=5)
+    x, y = O.synthetic_batch(ocfg)
+    gs = []
+    for flip in (False, True):
+        m = _model(ocfg, dtype=torch.bfloat16)
+        m.load_state_dict(st)
+        m.train()
+        m.hip_engine.row0_attention = first
+        torch.manual_seed(3)
+        loss = cross_entropy(m(x.to(DEV)), y.to(DEV))
+        if flip:
+            m.hip_engine.row0_attention = not first
+        loss.backward()
+        torch.cuda.synchronize()
+        gs.append(m.hip_engine.G.clone())
+    assert torch.isfinite(gs[0]).all()
+    assert torch.equal(gs[0], gs[1])
+
+
 def test_side_stream_weight_gradients_bitwise_equal():
     """Weight gradients on the side stream (engine.concurrent_wgrad) equal the in-order schedule bit for bit."""
     ocfg = O.make_config("micro", img=64, batch=4, blocks=2)
@@ -343,8 +373,9 @@ def test_two_stream_forward_bitwise_equal(dtype, img, train):
 
 def test_two_stream_forward_no_grad_bitwise_equal():
     """The inference forward (torch.no_grad: nothing saved, no masks kept) through the two-chain forward equals one
-    chain bit for bit, in eval and in train mode (dropout drawn, keep bits not stored)."""
-    ocfg = O.make_config("micro", img=224, batch=8, blocks=2)
+    chain bit for bit, in eval and in train mode (dropout drawn, keep bits not stored).  Five blocks: the four split
+    ones reuse the two ping-ponged buffer sets twice each."""
+    ocfg = O.make_config("micro", img=224, batch=8, blocks=5)
     ocfg.embedding_size, ocfg.num_heads = 768, 12
     st = O.init_state(ocfg, seed=10)
     x, _ = O.synthetic_batch(ocfg)
@@ -360,6 +391,56 @@ def test_two_stream_forward_no_grad_bitwise_equal():
                 out.append(m(x.to(DEV)).clone())
         torch.cuda.synchronize()
         assert torch.equal(out[0], out[1]), train
+
+
+def test_two_threads_forward_bitwise_and_no_option_mutation():
+    """Two models forwarding concurrently from two host threads: each thread's logits equal its solo
+    run bit for bit, and the two-chain forward never touches the process-wide option table (its 3/4-CU ring-attention
+    grid travels per call, vit_attn_fwd max_wgs, ABI 14) — polled while both threads run."""
+    import threading
+    ocfg = O.make_config("micro", img=224, batch=8, blocks=3)
+    ocfg.embedding_size, ocfg.num_heads = 768, 12
+    x, _ = O.synthetic_batch(ocfg)
+    xd = x.to(DEV)
+    models, solo = [], []
+    for i, streams in enumerate((2, 1)):
+        m = _model(ocfg, dtype=torch.bfloat16)
+        m.load_state_dict(O.init_state(ocfg, seed=20 + i))
+        m.eval()
+        m.hip_engine.fwd_streams = streams
+        with torch.no_grad():
+            solo.append(m(xd).clone())
+        models.append(m)
+    torch.cuda.synchronize()
+    assert _lib.get_option("attn_fwd_grid") == 0
+    results = [[], []]
+    errors = []
+
+    def run(i):
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st), torch.no_grad():
+                for _ in range(6):
+                    results[i].append(models[i](xd).clone())
+            st.synchronize()
+        except Exception as e:          # surfaced below
+            errors.append(e)
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in threads:
+        t.start()
+    seen = set()
+    while any(t.is_alive() for t in threads):
+        seen.add(_lib.get_option("attn_fwd_grid"))
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    assert seen <= {0}
+    for i in range(2):
+        assert len(results[i]) == 6
+        for r in results[i]:
+            assert torch.equal(r, solo[i]), i
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
@@ -482,7 +563,7 @@ def test_vit_base_full_depth_fp32_vs_fp64():
         inputs themselves carry the amplified rounding of the blocks below), and such flips must be rare (<= 1e-4 of
         the decisions; measured 1.2e-5; a wrong mask bit layout flips ~half of them); then
       * gradients vs fp64 evaluated with the engine's ReLU branches (the way the dropout masks are shared): every
-        tensor within max(2e-4, 8x the larger error of two valid fp32 summation orders — torch's and the oracle with
+        tensor within max(2e-4, 4x the larger error of two valid fp32 summation orders — torch's and the oracle with
         sequential-chain accumulation, this path's order — on the same branches), and the whole gradient vector
         within 2x the sequential-order sample (the rule of test_tiny_c1_fp32_vs_reference)."""
     ocfg = O.make_config("base", img=224, batch=8, num_classes=1000)
@@ -538,7 +619,7 @@ def test_vit_base_full_depth_fp32_vs_fp64():
                     float((gsq[k].double().reshape(-1) - r64).norm())) / n64
         e_own = float((ours[k].reshape(-1) - g64_own[k].reshape(-1)).norm()) / n64
         worst.append((e_ours / max(e_ref, 1e-12), k, e_ours, e_ref, e_own))
-        if e_ours > max(2e-4, 8 * e_ref):
+        if e_ours > max(2e-4, 4 * e_ref):          # the ViT-Tiny rule (round 6: was 8x; measured worst 2.16x)
             bad.append((k, e_ours, e_ref))
         cat["ours"].append(ours[k].reshape(-1))
         cat["seq"].append(gsq[k].double().reshape(-1))

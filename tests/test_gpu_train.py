@@ -87,6 +87,83 @@ def test_data_parallel_equals_gradient_accumulation():
         assert (v.cpu() - torch.from_numpy(ddp_state[k])).abs().max().item() < 1e-5, k
 
 
+def _keep_bits(m, x, seed):
+    """proj-dropout keep bits (VIT_MASK4 bytes) of block 0 in one training forward drawn under CPU seed `seed`."""
+    torch.manual_seed(seed)
+    _, tape = m.hip_engine.forward(x, True, save=True)
+    return tape.blocks[0][14].cpu().numpy()
+
+
+def _ddp_train_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "vision-transformer_amd")]
+    import torch.distributed as dist
+    from VisionTransformer import vit
+    from VisionTransformer.optim import FusedAdamW, cross_entropy
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = vit.VisionTransformer(_cfg()).cuda().train().enable_data_parallel()
+    opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    x, y = _batch(rank)
+    for _ in range(2):
+        loss = cross_entropy(m(x.cuda()), y.cuda())
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()} if rank == 0 else None
+    q.put((rank, m.hip_engine.dropout_rank, state, _keep_bits(m, x.cuda(), 7)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_train_mode_equals_per_rank_accumulation():
+    """Train mode, dropout on: a 2-rank data-parallel step equals one process that
+    accumulates the two ranks' micro-batches, each drawn under that rank's dropout stream (the same CPU RNG state,
+    the rank folded into the seed), within 1e-5 after two AdamW steps; and the two ranks' keep bits differ (before the
+    fix every replica applied the same masks)."""
+    import numpy as np
+    import torch.multiprocessing as mp
+    from VisionTransformer import vit
+    from VisionTransformer.optim import FusedAdamW, cross_entropy
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [0, 1]
+    ddp_state = res[0][2]
+    assert not np.array_equal(res[0][3], res[1][3])              # replicas draw different keep bits
+    torch.manual_seed(0)
+    m = vit.VisionTransformer(_cfg()).cuda().train()
+    opt = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    eng = m.hip_engine
+    for _ in range(2):
+        st = torch.get_rng_state()          # every rank draws its base seed from the same CPU RNG state
+        acc = None
+        for r in range(2):
+            torch.set_rng_state(st)
+            eng.dropout_rank = r
+            x, y = _batch(r)
+            loss = cross_entropy(m(x.cuda()), y.cuda())
+            for p in m.parameters():
+                p.grad = None
+            loss.backward()
+            g = eng.G.clone()
+            acc = g if acc is None else acc + g
+        eng.G.copy_(acc / 2)
+        opt.step()
+    for k, v in m.state_dict().items():
+        assert (v.cpu() - torch.from_numpy(ddp_state[k])).abs().max().item() < 1e-5, k
+    for r in range(2):                      # the single process reproduces each rank's masks exactly
+        eng.dropout_rank = r
+        assert np.array_equal(_keep_bits(m, _batch(r)[0].cuda(), 7), res[r][3]), r
+
+
 def test_train_loop_checkpoint_and_resume(tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "vision-transformer_amd"))
     import train as T

@@ -90,7 +90,10 @@ def main():
            for f, cs in fams.items()}
     kres = {k: dict(family=family(k), **derived(cs)) for k, cs in kers.items()}
     kres = dict(sorted(kres.items(), key=lambda kv: -kv[1].get("hbm_bytes_per_step", 0)))
+    sargs = os.environ.get("PMC_SCHEDULE_ARGS", "").strip()
     json.dump({"workload_key": key, "steps_divisor": steps,
+               "schedule": ("in-order (" + sargs + "): the schedule of bench.py's event-bracketed roofline step")
+               if sargs else "default (two forward chains + weight-gradient stream)",
                "method": "rocprofv3 --pmc, one counter group per pass over bench.py; per-kernel sums / steps; "
                          "FETCH_SIZE x2 (gfx950), WRITE_SIZE as reported; KiB -> bytes",
                "families": res, "kernels": kres}, open(out, "w"), indent=1)

@@ -59,6 +59,16 @@ def site_seed(base_seed, layer, site):
     return _hash_u32((base_seed * 0x632BE5AB + 0x1234567) & 0xFFFFFFFF, layer * 2 + site)
 
 
+def dropout_seed(base_seed, rank=0):
+    """Base dropout seed of one forward on data-parallel replica `rank`: the seed drawn from the CPU RNG, with the
+    rank hashed in for rank > 0 (rank 0 keeps the single-process seed, so a one-rank job is bitwise a plain run).
+    Each replica's masks are then a different counter-hash stream, as independent torch bernoulli draws per rank
+    would be (transformer.py:40,59 under an 8-way split of the batch)."""
+    if rank == 0:
+        return base_seed
+    return _hash_u32((base_seed ^ 0x5BD1E995) & 0xFFFFFFFF, 0x27D4EB2F + rank) & 0x7FFFFFFF
+
+
 class _Region:
     def __init__(self):
         self.size = 0
@@ -89,7 +99,7 @@ def head_split_for(m, n, k):
 class Tape:
     """Activations saved by a training forward."""
     __slots__ = ("B", "cols", "blocks", "z", "u", "gz", "zn", "mh", "rh", "seed", "training", "x_shape", "x_dtype",
-                 "x_grad", "pruned")
+                 "x_grad", "pruned", "row0")
 
 
 class Engine:
@@ -149,6 +159,10 @@ class Engine:
         # kernels with the output gradient zero outside row 0 (A/B runs; set it between steps, not between a forward
         # and its backward)
         self.row0_attention = True
+        # data-parallel replica index folded into the dropout seed (enable_data_parallel sets the group rank): every
+        # rank draws the same base seed from its identically seeded CPU RNG, so without it all replicas would apply
+        # the same keep masks to different images.  0 (rank 0, single process) leaves the seed unchanged.
+        self.dropout_rank = 0
 
     # ------------------------------------------------------------------------------------------------------------
     # layout
@@ -463,7 +477,7 @@ class Engine:
         es = 2 if dt == torch.bfloat16 else 4
         prm = self.params
         mk = self._mark
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training else 0
+        seed = dropout_seed(int(torch.randint(0, 2 ** 31 - 1, (1,)).item()), self.dropout_rank) if training else 0
         tape = Tape() if save else None
 
         blocks = []
@@ -496,6 +510,9 @@ class Engine:
             tape.x_shape, tape.x_dtype = tuple(x.shape), x.dtype
             tape.z, tape.u, tape.gz, tape.zn, tape.mh, tape.rh = z, u, gz, zn, mh, rh
             tape.seed, tape.training, tape.pruned = seed, training, prune
+            # which attention the pruned block's forward ran (query 0 alone, or the full kernels): its backward must
+            # be the matching one whatever row0_attention says by then (the row-0 forward writes only rows b*T)
+            tape.row0 = prune and self.row0_attention and not want_probs
         return logits, tape
 
     def _block_bufs(self, B, training, save, dev):
@@ -558,30 +575,41 @@ class Engine:
         names = ("a1", "m1", "r1", "qkv", "o", "o32", "lse", "x_mid", "a2", "m2", "r2", "h", "hm", "pm", "fm")
         # the ring attention forward of one chain on 3/4 of the CUs, so the other chain's GEMMs run beside it instead
         # of waiting for the whole latency-bound kernel (one box, interleaved: 30.50 -> 30.19 ms/step; 1/2 and 7/8 of
-        # the CUs gain less) — unless the caller set attn_fwd_grid itself
-        grid_opt = _lib.get_option("attn_fwd_grid")
-        if grid_opt == 0:
-            _lib.set_option("attn_fwd_grid", max(1, torch.cuda.get_device_properties(dev).multi_processor_count * 3 // 4))
+        # the CUs gain less) — unless the caller set the attn_fwd_grid option itself.  Passed per call (vit_attn_fwd's
+        # max_wgs, ABI 14): no process-wide state changes, so concurrent forwards on other threads are unaffected.
+        wgs = 0
+        if _lib.get_option("attn_fwd_grid") == 0:
+            wgs = max(1, torch.cuda.get_device_properties(dev).multi_processor_count * 3 // 4)
         self._split_fwd = True
         # the pruned last block runs whole-batch after the join: split, its B token-0 rows would become two GEMMs of
         # B/2 rows (below the 256-row tile: the slow small-M kernels)
         nsplit = L - 1 if prune else L
+        # without a tape (no_grad / eval) nothing outlives the next block: two buffer sets, ping-ponged.  Each chain
+        # reads and writes only its own rows, in order on its own stream, so block l + 2 may overwrite block l's rows
+        # of a chain once that chain's block l + 1 consumed them (fresh sets per block, each recorded on
+        # both streams, let the caching allocator hold up to L blocks of activations while the host runs ahead)
+        ping = None if save else [self._block_bufs(B, training, save, dev) for _ in range(2)]
+        for t in ([xcur] if save else [xcur] + [t for bs in ping for t in bs.values()]):
+            for st in streams:
+                t.record_stream(st)
         try:
             for l in range(nsplit):
-                bufs = self._block_bufs(B, training, save, dev)
-                for t in list(bufs.values()) + [xcur]:
-                    for st in streams:
-                        t.record_stream(st)
+                if save:
+                    bufs = self._block_bufs(B, training, save, dev)
+                    for t in bufs.values():
+                        for st in streams:
+                            t.record_stream(st)
+                else:
+                    bufs = ping[l % 2]
                 for i, st in enumerate(streams):
                     with torch.cuda.stream(st):
                         self.block_forward(l, xcur[i * Mh:(i + 1) * Mh], Bh, training, seed, save, False, False,
-                                           bufs=bufs, b0=i * Bh)
+                                           bufs=bufs, b0=i * Bh, attn_wgs=wgs)
                 if save:
                     blocks.append((xcur,) + tuple(bufs.get(n) for n in names))
                 xcur = bufs["x_out"]
         finally:
             self._split_fwd = False
-            _lib.set_option("attn_fwd_grid", grid_opt)
         pre = None
         if nsplit < L and self.row0_attention:
             # the pruned block's ln1 and K / V GEMM are whole-row work: per chain too
@@ -610,7 +638,7 @@ class Engine:
         return xcur
 
     def block_forward(self, l, x_in, B, training, seed, save, want_probs=False, pr=False, bufs=None, b0=0,
-                      pre=None):
+                      pre=None, attn_wgs=0):
         """Block l (transformer.py:76-79) on x_in [B*T, D] (compute dtype): x_mid = x_in + drop(MHA(ln1(x_in))),
         x_out = x_mid + drop(FFN(ln2(x_mid))).  `pr`: the post-attention part on the B token-0 rows only (the pruned
         last block).  Returns (x_out, saved): `saved` is what block_backward needs (None unless `save`).
@@ -674,7 +702,8 @@ class Engine:
                 o32 = rows("o32") if bufs is not None else torch.empty(M, D, dtype=torch.float32, device=dev)
             mk("attn_fwd", 0, 4.0 * B * H * T * T * hd, 4 * M * D * es + 4 * B * H * T + (4 * M * D if o32 is not None
                                                                                          else 0))
-            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, o=rows("o"), lse=rows("lse"), probs=probs, o32=o32)
+            o, lse = _ops.attn_fwd(qkv, B, T, H, hd, self.scale, o=rows("o"), lse=rows("lse"), probs=probs, o32=o32,
+                                   max_wgs=attn_wgs)
             mk("attn_fwd", 1)
         blk.multi_head.attention_probs = probs
         blk.multi_head._probs_skipped = probs is None       # a later read warns once (transformer.py)
@@ -847,7 +876,8 @@ class Engine:
                 break
             prev_mask = tape.blocks[l - 1][15] if (tape.training and l > 0) else None
             dx, g1n = self.block_backward(l, tape.blocks[l], dx, g1, g1_summed, beta, req, side, tape.training, B,
-                                          pruned and l == L - 1, chain_prev=l > 0, prev_mask=prev_mask)
+                                          pruned and l == L - 1, chain_prev=l > 0, prev_mask=prev_mask,
+                                          row0=tape.row0 and l == L - 1)
             g1_summed = l > 0
             self._bucket_ready(self.block_range[l], side)
             g1 = g1n if g1n is not None else dx
@@ -878,13 +908,16 @@ class Engine:
         return dimg
 
     def block_backward(self, l, saved, dx, g1, g1_summed, beta, req, side, training, B, pr=False, chain_prev=False,
-                       prev_mask=None):
+                       prev_mask=None, row0=None):
         """Backward of block l from d(x_out) = dx and g1 = the fc2-dropout-masked dx (dx itself in eval).  Writes the
         block's weight gradients into the flat buffer (beta: 0 overwrite / 1 accumulate; req: which regions want a
         gradient) and returns (dx_in, g1n).  `chain_prev`: there is a block l-1 below, so the ln1 backward also emits
         block l-1's fc2 bias-gradient column sums and — in training, from its keep bits `prev_mask` — g1n, the next
         block's masked gradient (None otherwise).  `g1_summed`: this block's fc2 bias gradient was already summed by
-        the block above.  `pr`: the pruned last block (dx / g1 are its B token-0 rows)."""
+        the block above.  `pr`: the pruned last block (dx / g1 are its B token-0 rows).  `row0`: its forward ran the
+        query-0 attention (Tape.row0; None: pr and self.row0_attention, for direct callers)."""
+        if row0 is None:
+            row0 = pr and self.row0_attention
         D, T, H, hd, dt = self.D, self.T, self.H, self.hd, self.dtype
         M = B * T
         gw = self.gw
@@ -939,7 +972,7 @@ class Engine:
             dxm_full = self._token_rows("dxm", M, D, dt, T, dev)
             _ops.copy2d(dx_mid, D, dxm_full, T * D, B, D)
             dx_mid = dxm_full
-        if pr and self.row0_attention:
+        if row0:
             # attention backward from the row-0 output gradients alone (the forward computed row 0 only): dQ row 0, all
             # of dK / dV; the dQ rows 1..T-1 of this buffer are never written, so they stay zero for the dgrad /
             # wgrad GEMMs below
@@ -967,7 +1000,7 @@ class Engine:
             mk("attn_bwd", 1)
         wq = self.ww[f"{l}.qkv_w"]
         da1 = torch.empty(M, D, dtype=dt, device=dev)
-        if pr and self.row0_attention:
+        if row0:
             # dQ is zero outside the token-0 rows: the K / V part over every row, the Q part over the B token-0 rows
             # (weight gradient: its own K = B GEMM; input gradient: added onto those rows of da1 by the residual
             # epilogue, in place)

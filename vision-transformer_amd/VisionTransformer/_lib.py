@@ -10,7 +10,7 @@ import os
 import torch  # noqa: F401  (must be imported first: provides the HIP runtime the library binds to)
 
 LIB_PATH = os.environ.get("VIT_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvit_hip.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 F32, BF16, MASK4 = 0, 1, 2
 FLAG_SHARED_CUS = 1          # VIT_FLAG_SHARED_CUS (vit_hip.h)
@@ -70,7 +70,7 @@ _SIGS = {
     "vit_layernorm_bwd_parts": (_I64, [_I64, _I64]),
     "vit_layernorm_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _F, _U32, _P, _P, _I32, _I64,
                                          _I64, _I32, _P]),
-    "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P]),
+    "vit_attn_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _I64, _P]),
     "vit_attn_bwd_uses_o32": (ctypes.c_int, [_I64, _I64, _I64, _I64, _I32]),
     "vit_attn_bwd_workspace_bytes": (_I64, [_I64, _I64, _I64, _I64, _I32]),
     "vit_attn_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _I32, _P, _I32, _P]),

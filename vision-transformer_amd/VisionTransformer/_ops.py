@@ -170,15 +170,16 @@ def layernorm_bwd(dy, x, gamma, mean, rstd, dx_out, dres=None, drop_out=None, dr
     return partial
 
 
-def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, o32=None, stream=None):
+def attn_fwd(qkv, B, T, H, hd, scale, o=None, lse=None, probs=None, o32=None, max_wgs=0, stream=None):
     """o = softmax(scale Q K^T) V per head; `o32` (bf16 only): also store O unrounded (fp32) for attn_bwd's delta
-    where attn_bwd_uses_o32() says the backward takes it."""
+    where attn_bwd_uses_o32() says the backward takes it.  `max_wgs` > 0: at most that many workgroups for the
+    persistent ring forward, for this call only (0: automatic / the library option)."""
     _need_cuda(qkv)
     D = H * hd
     o = torch.empty(B * T, D, dtype=qkv.dtype, device=qkv.device) if o is None else o
     lse = torch.empty(B, H, T, dtype=torch.float32, device=qkv.device) if lse is None else lse
     _lib.call("vit_attn_fwd", _ptr(qkv), _ptr(o), _ptr(o32), _ptr(lse), _ptr(probs), B, T, H, hd, scale,
-              dtype_code(qkv), _stream(stream))
+              dtype_code(qkv), int(max_wgs), _stream(stream))
     return o, lse
 
 

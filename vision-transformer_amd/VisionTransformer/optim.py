@@ -123,7 +123,8 @@ class FusedAdamW(torch.optim.Optimizer):
                     # entries keep every tabled tensor alive; the raw shadow list is what the identity check compares
                     tab = (self._version, list(ps), [p.grad for p in ps], [shadow_of(p) for p in ps], dev_tab, n,
                            sdt, entries, [p.data_ptr() for p in ps],
-                           [(self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"]) for p in ps])
+                           [(self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"]) for p in ps],
+                           [p.grad.data_ptr() for p in ps])
                     self._tables[key] = tab
                 dev_tab, n, sdt = tab[4], tab[5], tab[6]
                 _ops.adamw(dev_tab, n, group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** t,
@@ -132,16 +133,17 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def _table_valid(self, tab, ps):
         """Same optimizer version, same parameters, every parameter still holds the same .grad tensor object and the
-        same moment tensor objects as when the table was built, and no parameter's storage moved (`p.data = ...`
-        re-points storage without changing any object identity).  One data_ptr() per parameter plus
+        same moment tensor objects as when the table was built, and no parameter's or gradient's storage moved (`p.data = ...`
+        re-points storage without changing any object identity).  Two data_ptr() per parameter plus
         identity checks: this runs every step.  The engine's shadows change only when it rebuilds its buffers, and
         then every gradient view is a new object too."""
-        ver, tps, grads, ptrs, moments = tab[0], tab[1], tab[2], tab[8], tab[9]
+        ver, tps, grads, ptrs, moments, gptrs = tab[0], tab[1], tab[2], tab[8], tab[9], tab[10]
         if ver != self._version or len(tps) != len(ps):
             return False
         state = self.state
-        for a, b, g, ptr, (m, v) in zip(tps, ps, grads, ptrs, moments):
-            if a is not b or a.grad is not g or a.data_ptr() != ptr:
+        for a, b, g, ptr, (m, v), gp in zip(tps, ps, grads, ptrs, moments, gptrs):
+            # the gradient's storage too: `p.grad.data = t` / `p.grad.set_(...)` keep the .grad object (ADVICE r5)
+            if a is not b or a.grad is not g or a.data_ptr() != ptr or g.data_ptr() != gp:
                 return False
             st = state[a]
             if st["exp_avg"] is not m or st["exp_avg_sq"] is not v:

@@ -119,6 +119,8 @@ class VisionTransformer(nn.Module):
         # "shared": the backward's kernels launch one workgroup per item instead of a persistent one-per-CU grid
         # (VIT_FLAG_SHARED_CUS, vit_hip.h), so RCCL's all-reduce kernels beside them never wait for a whole grid
         eng.shared_cus = eng.ddp_enabled and launch_mode == "shared"
+        # each replica draws its own dropout masks (the rank is folded into the forward's dropout seed)
+        eng.dropout_rank = dist.get_rank(group) if eng.ddp_enabled else 0
         return self
 
     # the engine holds a weakref to its model and views of the parameters: never copy or pickle it (a deep copy or

@@ -1877,7 +1877,7 @@ bool use_mfma(int32_t dtype, int64_t hd) { return dtype == VIT_BF16 && hd == HD;
 }  // namespace
 
 extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, float* probs, int64_t B, int64_t T,
-                            int64_t H, int64_t hd, float scale, int32_t dtype, void* stream) {
+                            int64_t H, int64_t hd, float scale, int32_t dtype, int64_t max_wgs, void* stream) {
   VIT_REQUIRE(qkv && o && lse && B > 0 && T > 0 && H > 0 && hd > 0, "vit_attn_fwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && probs == nullptr) {
@@ -1885,7 +1885,9 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
     if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING)) {
       const int64_t items = B * H;
       unsigned grid = (unsigned)std::min<int64_t>(items, vit_cu_count());
-      if (const int64_t gopt = vit::opt(vit::OPT_ATTN_FWD_GRID)) grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, gopt));
+      // per call (ABI 14: max_wgs > 0, e.g. one chain of the two-stream forward on 3/4 of the CUs), else the option
+      const int64_t gopt = max_wgs > 0 ? max_wgs : vit::opt(vit::OPT_ATTN_FWD_GRID);
+      if (gopt > 0) grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, gopt));
 #define RING(NT) \
   attn_fwd_ring<NT><<<grid, NT * 64, 0, s>>>((const bf16_t*)qkv, (bf16_t*)o, o32, lse, T, H, items, scale)
       switch ((int)((T + 15) / 16)) {

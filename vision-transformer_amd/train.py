@@ -88,7 +88,9 @@ def evaluate(model, test_loader, eval_func, avg=None):
     """Mean over batches of eval_func(labels, argmax(logits)) (train.py:29-44).
 
     A partial last batch is padded to the model's batch size (the CLS parameter is batch-shaped, vit.py:32,41) and
-    only its real rows are scored; the reference would raise there.
+    only its real rows are scored; the reference would raise there.  With such a batch the score is eval_func over
+    the whole set (every sample weighted once, the same value a data-parallel run returns) instead of the mean of
+    per-batch scores, which is kept whenever every batch is full (the reference's only working case).
 
     Under data parallelism (an initialized process group of world size > 1) every rank scores its own shard of the test
     set, the (label, prediction) pairs of all ranks are gathered, and eval_func runs once over the whole set, so every
@@ -117,10 +119,16 @@ def evaluate(model, test_loader, eval_func, avg=None):
         n += 1
     model.train()
     rank, world = _rank_world()
-    if world == 1:
-        return score / max(n, 1)
     lab = torch.cat(labs) if labs else torch.zeros(0, dtype=torch.long)
     pred = torch.cat(preds) if preds else torch.zeros(0, dtype=torch.long)
+    if world == 1:
+        if pad_to is None or all(len(v) == pad_to for v in labs):
+            return score / max(n, 1)             # the reference's mean of per-batch scores (full batches only)
+        # a padded partial batch: score the whole set once, as the data-parallel case does, so the same model reports
+        # the same score on one rank and on many (a mean of per-batch scores would weight the partial batch fully)
+        if avg is None:
+            return float(eval_func(lab, pred))
+        return float(eval_func(lab, pred, average=avg, zero_division=0.0))
     s = _sampler_of(test_loader)
     if isinstance(s, torch.utils.data.DistributedSampler) and not s.drop_last:
         keep = len(range(rank, len(s.dataset), world))           # the shard's samples before the padding
@@ -171,6 +179,12 @@ class SyntheticImages(torch.utils.data.Dataset):
         return torch.randn(self.shape, generator=g), int(torch.randint(0, self.classes, (1,), generator=g))
 
 
+def replica_seed(rank, base=0):
+    """CPU RNG seed of data-parallel replica `rank` after the identically seeded init (host path): rank 0 keeps
+    `base`, so a one-rank job draws what a plain run draws."""
+    return base if rank == 0 else (base + 0x9E3779B1 * rank) % (2 ** 63 - 1)
+
+
 def _rank_world():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -210,8 +224,11 @@ def train(configs, train_loader, test_loader, epochs, eval_iter, log_dir, checkp
     if world > 1:
         if device == "cpu":      # host path: standard autograd, so torch's own DDP (gloo) applies
             net = torch.nn.parallel.DistributedDataParallel(model)
+            # the host dropout (F.dropout, transformer.py:47,59) draws from the CPU RNG, seeded identically above
+            # for identical init: give each replica its own stream, or all ranks mask their images alike
+            torch.manual_seed(replica_seed(rank))
         else:
-            model.enable_data_parallel()
+            model.enable_data_parallel()      # the engine folds the rank into its dropout seed
     writer = _writer(log_dir) if rank == 0 else None
     running_loss = 0.0
     for epoch in range(saved_epoch, epochs + 1):
