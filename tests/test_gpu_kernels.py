@@ -661,41 +661,6 @@ def test_attention_bwd_fused_matches_split(libopt, T):
     assert (fused.float() - split.float()).abs().max().item() <= 2e-2 * max(1.0, g.abs().max().item())
 
 
-@pytest.mark.parametrize("T", [1, 17, 31, 33, 64, 65, 100, 128, 160, 197, 209, 224, 256])
-@pytest.mark.parametrize("amp", [0.5, 2.0])
-def test_attention_bwd_w16(libopt, T, amp):
-    """attn_bwd_w16 (round 6: 16 keys per wave, 2 ceil(T/32) waves, <= 128 VGPRs) against the same-rounding fp64
-    reference at the bf16 kernel gate (2e-2 of each of dQ / dK / dV), including saturated softmax rows (amp 2: the
-    in-kernel delta from P and dP must stay exact); within the same gate of attn_bwd_fused; bitwise the same over
-    persistent grids of 1 / 7 workgroups (more items than workgroups) and the shared-CU launch."""
-    torch.manual_seed(T + int(10 * amp))
-    B, H, hd = 3, 5, 64
-    D = H * hd
-    scale = 8.0
-    qkv = (torch.randn(B * T, 3 * D, device=DEV) * amp).bfloat16()
-    o, lse = _ops.attn_fwd(qkv, B, T, H, hd, scale)
-    d_o = torch.randn(B * T, D, device=DEV).bfloat16()
-    old_ = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale)
-    libopt("attn_bwd_w16", 1)
-    new_ = _ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale)
-    ref = _attn_flash_grads(qkv, d_o, B, T, H, hd, scale)
-    floor = 1e-3 * float(ref.norm())
-    for name, sl in (("dQ", slice(0, D)), ("dK", slice(D, 2 * D)), ("dV", slice(2 * D, 3 * D))):
-        r = ref[:, sl]
-        den = max(float(r.norm()), floor)
-        e_new = float((new_[:, sl].double() - r).norm()) / den
-        e_old = float((old_[:, sl].double() - r).norm()) / den
-        print(f"{name}: w16 {e_new:.2e}, fused {e_old:.2e}")
-        # the bf16 kernel gate, or no worse than twice the shipped kernel where that one exceeds it (T = 1 at amp 2:
-        # dQ = dK = 0 exactly, both kernels leave P = 1 - eps rounding residue of a 370-wide exp2 argument)
-        assert e_new <= max(2e-2, 2 * e_old), (name, e_new, e_old)
-    for grid in (1, 7):
-        libopt("attn_bwd_grid", grid)
-        assert torch.equal(_ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale), new_), grid
-    libopt("attn_bwd_grid", 0)
-    assert torch.equal(_ops.attn_bwd(qkv, o, d_o, lse, B, T, H, hd, scale, shared_cus=True), new_)
-
-
 @pytest.mark.parametrize("grid", [0, 7, 100])
 def test_attention_bwd_shared_cus_bitwise(libopt, grid):
     """VIT_FLAG_SHARED_CUS (one workgroup per (image, head) instead of the persistent grid that stages the next item

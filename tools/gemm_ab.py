@@ -26,6 +26,10 @@ SHAPES = {  # name: m, n, k, a_kcontig, b_kcontig, epilogue
     "wgrad_fc1": (4 * D, D, M, False, False, "wgrad"), "wgrad_fc2": (D, 4 * D, M, False, False, "wgrad"),
     "wgrad_qkv": (3 * D, D, M, False, False, "wgrad"), "wgrad_proj": (D, D, M, False, False, "wgrad"),
     "sq8192": (8192, 8192, 8192, True, True, None),
+    # the proj / fc2 epilogue's parts (round 6): plain, bias + residual, + dropout, + dropout keep bits (the engine's)
+    "fwd_proj_plain": (M, D, D, True, True, None), "fwd_proj_br": (M, D, D, True, True, "br"),
+    "fwd_proj_bdrm": (M, D, D, True, True, "bdrm"), "fwd_fc2_plain": (M, D, 4 * D, True, True, None),
+    "fwd_fc2_br": (M, D, 4 * D, True, True, "br"), "fwd_fc2_bdrm": (M, D, 4 * D, True, True, "bdrm"),
     # the same square GEMM in the dgrad (A k-contiguous, B row-strided) and weight-gradient (both row-strided, f32 out)
     # operand layouts: what the transposed LDS reads cost the k-loop
     "sq8192_kr": (8192, 8192, 8192, True, False, None), "sq8192_rr": (8192, 8192, 8192, False, False, "wgrad"),
@@ -57,7 +61,7 @@ def desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res, mask):
     d.in_dtype = _lib.BF16
     d.out_dtype = _lib.F32 if epi == "wgrad" else _lib.BF16
     d.alpha, d.beta = 1.0, 0.0
-    if epi in ("bias_relu", "bias_relu_m", "bdr"):
+    if epi in ("bias_relu", "bias_relu_m", "bdr", "bdrm", "br"):
         d.bias = bias.data_ptr()
     if epi in ("bias_relu", "bias_relu_m"):
         d.act = _lib.ACT_RELU
@@ -67,9 +71,12 @@ def desc(a, b, c, m, n, k, akc, bkc, epi, split, ws, aux, bias, res, mask):
         d.aux, d.ldaux, d.aux_dtype = mask.data_ptr(), 0, _lib.MASK4
     if epi == "aux":
         d.aux, d.ldaux, d.aux_dtype = aux.data_ptr(), n, _lib.BF16
-    if epi == "bdr":
+    if epi in ("bdr", "bdrm", "br"):
         d.res, d.ldres, d.res_dtype = res.data_ptr(), n, _lib.BF16
+    if epi in ("bdr", "bdrm"):
         d.dropout_p, d.dropout_seed = 0.2, 7
+    if epi == "bdrm":
+        d.mask_out = mask.data_ptr()
     d.split_k = split
     d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel() * 4
     return d

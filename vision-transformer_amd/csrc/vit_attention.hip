@@ -1172,358 +1172,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Fused backward, 16 keys per wave (round 6; option "attn_bwd_w16"): the algorithm of attn_bwd_fused (delta from the
-// fp32 P and dP, dQ from a dS^T image, the same three-stage software pipeline over 32-query blocks, the next item
-// staged into blocks as they die) with half the per-wave state, so twice the waves fit a CU: 2 NQB waves (14 at
-// T = 197, 4 per SIMD instead of 2) at <= 128 VGPRs, each owning 16 keys instead of 32.  The kernel is latency-bound
-// (MFMA busy 0.18 at 2 waves per SIMD); the extra waves hide the LDS / MFMA / exp dependency chains of each other.
-// All products are v_mfma_f32_16x16x32_bf16 with the keys on the lanes of the result:
-//   S, dP   [32 queries x 16 keys]: two 16x16 tiles whose rows interleave the queries (tile qt, row m <-> query
-//           8 (m >> 2) + 4 qt + (m & 3)), so lane (g = lane / 16, key lane & 15) holds the 8 consecutive queries 8g..8g+7;
-//   dV^T, dK^T [64 hd x 16 keys] += dO^T P, Q^T dS: A = a transposed read of the dO / Q block (rows 8g..8g+7), B = the
-//           lane's own packed P / dS — no LDS round trip for P; each lane ends with 4 consecutive hd of its key (8-B
-//           stores);
-//   delta   the 16 key lanes of each row summed by a fixed DPP tree, the waves' partials in wave order;
-//   dQ      as attn_bwd_fused (8 tiles of 16 x 16 over all keys, on the last 8 waves).
-// ---------------------------------------------------------------------------------------------------------------
-#ifndef W16_PEEL
-#define W16_PEEL 0
-#endif
-VIT_DEV f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
-
-// u[j] <- sum of u[j] over the 16 lanes of the lane's 16-lane row (fixed pairing; lane 0 of a row holds a fixed-order
-// sum: deterministic).  A DPP read needs 2 wait states after the VALU write of its register: the s_nop covers the first
-// step, later steps read registers written 8 instructions earlier.
-VIT_DEV void rowsum16x8(float (&u)[8]) {
-#define VIT_DPP16_ADD8(CTRL)                                                                                      \
-  asm volatile("s_nop 1\n\t"                                                                                    \
-               "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %4, %4, %4 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %5, %5, %5 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %6, %6, %6 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                             \
-               "v_add_f32_dpp %7, %7, %7 " CTRL " row_mask:0xf bank_mask:0xf"                                   \
-               : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]))
-  VIT_DPP16_ADD8("row_ror:8");
-  VIT_DPP16_ADD8("row_ror:4");
-  VIT_DPP16_ADD8("quad_perm:[2,3,0,1]");
-  VIT_DPP16_ADD8("quad_perm:[1,0,3,2]");
-#undef VIT_DPP16_ADD8
-}
-
-template <int NQB>
-__global__ __launch_bounds__(NQB * 128, 1) void attn_bwd_w16(const bf16_t* __restrict__ qkv,
-                                                            const bf16_t* __restrict__ d_o,
-                                                            const float* __restrict__ lse, bf16_t* __restrict__ dqkv,
-                                                            int64_t Tn64, int64_t H, int64_t items, float scale) {
-  constexpr int Tp = NQB * 32;                        // T rounded up to 32: query blocks and image rows
-  constexpr int NW = 2 * NQB;                         // waves: wave w owns keys 16w .. 16w + 15
-  constexpr int NT = NW * 64;
-  constexpr int nqb = NQB;
-  constexpr int IMG = Tp * HD;
-  constexpr int DST = Tp * 32;                        // dS^T image [Tp keys][32 queries] (attn_bwd_fused's layout)
-  constexpr int QRS = HD + 4;
-  constexpr int QST = 32 * QRS;
-  constexpr int NF = Tp + 2 * NW * 32 + NW * 32;      // lse2 [Tp], delta partials [2][NW][32], per-wave delta [NW][32]
-  constexpr bool VLDS = (4 * IMG + 2 * DST + 2 * QST) * 2 + NF * 4 <= 160 * 1024;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[(VLDS ? 4 : 3) * IMG + 2 * DST + 2 * QST + 2 * NF];
-  bf16_t* Ks = smem;
-  bf16_t* Qs = Ks + IMG;
-  bf16_t* Gs = Qs + IMG;
-  bf16_t* dSt = Gs + IMG;                              // [2][Tp][32]
-  bf16_t* dQs = dSt + 2 * DST;                         // [2][32][QRS]
-  bf16_t* Vs = dQs + 2 * QST;                          // [Tp][64] when VLDS
-  float* lse2s = reinterpret_cast<float*>(Vs + (VLDS ? IMG : 0));
-  float* dpart = lse2s + Tp;                           // [2][NW][32]
-  float* dwav = dpart + 2 * NW * 32;                   // [NW][32]
-
-  const int tid = threadIdx.x, lane = tid & 63, lk = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int Tn = (int)Tn64;
-  const int nkw = (Tn + 15) >> 4;                      // waves that own keys
-  const bool kact = wave < nkw;
-  const int key = wave * 16 + lk;                      // < Tp
-  const float kbias = key < Tn ? 0.f : -INFINITY;
-  const int64_t D = H * HD, ld = 3 * D;
-  const float c2 = scale * LOG2E;
-  // dQ tiles: the last 8 waves take one each (waves with few or no keys among them); fewer waves loop
-  const int dq_first = NW >= 8 ? wave - (NW - 8) : wave;
-  constexpr int dq_step = NW >= 8 ? 8 : NW;
-
-  // S / dP A operand: query row rl = 8 (lk >> 2) + 4 qt + (lk & 3) of a 32-row block, 16-B chunk 4 s + g
-  int qro_[2][2];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int rl = 8 * (lk >> 2) + 4 * qt + (lk & 3);
-      qro_[qt][s] = rl * HD + (((4 * s + g) ^ aswz(rl)) << 3);
-    }
-  auto qro = [&](int qt, int s) { return qro_[qt][s]; };
-  // transposed reads of a 32-row block: X[8g + j][16 nt + lk], j = 0..7 (col_frag16's addressing)
-  int cfo_[4][2];
-  {
-    const int q = lk >> 2, pp = lk & 3;
-    const int ra = 8 * g + q, rb = ra + 4;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int col = 16 * nt + 4 * pp, c = col >> 3;
-      cfo_[nt][0] = ra * HD + ((c ^ aswz(ra)) << 3) + (col & 7);
-      cfo_[nt][1] = rb * HD + ((c ^ aswz(rb)) << 3) + (col & 7);
-    }
-  }
-  auto cfo = [&](int nt, int half) { return cfo_[nt][half]; };
-  auto trd = [&](const bf16_t* base, int o1, int o2) {
-    s16x4 lo = tr_read(base + o1);
-    s16x4 hi = tr_read(base + o2);
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  };
-  auto rrd = [&](const bf16_t* base, int o) {
-    return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const s16x8*>(base + o));
-  };
-  float lreg = 0.f;
-  auto load_lse = [&](int64_t it_) {
-    const int t_ = remat(tid);
-    if (t_ < Tn) lreg = lse[it_ * Tn + t_];
-  };
-  auto dma_slice = [&](const bf16_t* base, int64_t row0, int64_t ldx, int64_t col0, bf16_t* img) {
-    for (int pc = wave; pc < Tp / 8; pc += NW) dma_piece(base, row0, ldx, col0, Tn, img, pc, lane);
-  };
-  // dS^T rows of keys no wave owns and the delta partials of waves without keys are never written: zero them once
-  // (dQ sums over all Tp key rows, delta over all NW waves: branch-free, +0 exactly)
-  for (int i = tid; i < 2 * DST / 8; i += NT) *reinterpret_cast<uint4*>(dSt + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
-  for (int i = tid; i < 2 * NW * 32; i += NT) dpart[i] = 0.f;
-
-  int64_t item = blockIdx.x;
-  if (item < items) {
-    const int64_t b = item / H, h = item % H;
-    dma_slice(qkv, b * Tn, ld, D + h * HD, Ks);
-    dma_slice(qkv, b * Tn, ld, h * HD, Qs);
-    dma_slice(d_o, b * Tn, D, h * HD, Gs);
-    if (VLDS) dma_slice(qkv, b * Tn, ld, 2 * D + h * HD, Vs);
-    load_lse(item);
-  }
-#pragma unroll 1
-  for (; item < items; item += gridDim.x) {
-    const int64_t b = item / H, h = item % H;
-    const int64_t nxt = item + gridDim.x;
-    const bool more = nxt < items;
-    const int64_t sb_ = more ? nxt / H : b, sh_ = more ? nxt % H : h;   // staged next (or this item again: dead blocks)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / V DMA, lse
-    {
-      const int t_ = remat(tid);
-      if (t_ < Tp) lse2s[t_] = t_ < Tn ? lreg * LOG2E : INFINITY;
-    }
-    __syncthreads();
-    bf16x8_t kf[2], vf[2];
-    {
-      const int kr = wave * 16 + lk;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int o = kr * HD + (((4 * s + g) ^ aswz(kr)) << 3);
-        kf[s] = rrd(Ks, o);
-        if (VLDS) {
-          vf[s] = rrd(Vs, o);
-        } else {
-          s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-          if (kr < Tn) v = *reinterpret_cast<const s16x8*>(qkv + (b * Tn + kr) * ld + 2 * D + h * HD + 32 * s + 8 * g);
-          vf[s] = __builtin_bit_cast(bf16x8_t, v);
-        }
-      }
-    }
-    f32x4 dk[4], dv[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) dk[nt] = dv[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float pc[8], dpc[8];                               // P, dP of queries q0 + 8g + j for this lane's key
-
-    // front(qb): S, dP -> P; dV^T += dO^T P; this wave's partial delta over its 16 keys -> dpart[qb & 1][wave]
-    auto front = [&](int qb) {
-      if (!kact) return;
-      const int q0 = qb * 32;
-      const bf16_t* Qb = Qs + q0 * HD;
-      const bf16_t* Gb = Gs + q0 * HD;
-      f32x4 sacc[2], pacc[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) sacc[qt] = pacc[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          const int o = qro(qt, s);
-          sacc[qt] = mfma16(rrd(Qb, o), kf[s], sacc[qt]);                  // S[q][key]
-          pacc[qt] = mfma16(rrd(Gb, o), vf[s], pacc[qt]);                  // dP[q][key]
-        }
-      const f32x4 l0 = *reinterpret_cast<const f32x4*>(lse2s + q0 + 8 * g);
-      const f32x4 l1 = *reinterpret_cast<const f32x4*>(lse2s + q0 + 8 * g + 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        // queries >= T have lse2 = +inf, keys >= T kbias = -inf -> P = 0 exactly
-        pc[i] = __builtin_amdgcn_exp2f(sacc[0][i] * c2 - l0[i] + kbias);
-        pc[4 + i] = __builtin_amdgcn_exp2f(sacc[1][i] * c2 - l1[i] + kbias);
-        dpc[i] = pacc[0][i];
-        dpc[4 + i] = pacc[1][i];
-      }
-      const bf16x8_t p8 = pack8(pc);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) dv[nt] = mfma16(trd(Gb, cfo(nt, 0), cfo(nt, 1)), p8, dv[nt]);
-      float u[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = pc[j] * dpc[j];
-      rowsum16x8(u);
-      if (remat(lk) == 0) {
-        float* dp = dpart + (qb & 1) * NW * 32 + wave * 32 + 8 * g;
-        *reinterpret_cast<f32x4*>(dp) = f32x4{u[0], u[1], u[2], u[3]};
-        *reinterpret_cast<f32x4*>(dp + 4) = f32x4{u[4], u[5], u[6], u[7]};
-      }
-    };
-
-    // back(qb): delta (the key waves' partials in wave order) -> dS -> dK^T += Q^T dS; dS^T -> dSt[qb & 1]
-    auto back = [&](int qb) {
-      if (!kact) return;
-      const int q0 = qb * 32;
-      const bf16_t* Qb = Qs + q0 * HD;
-      const float* dp = dpart + (qb & 1) * NW * 32 + (lane & 31);
-      float dsum = dp[0];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) dsum += dp[w * 32];    // waves without keys: zero partials (set once below)
-      float* dw = dwav + wave * 32;
-      dw[lane & 31] = dsum;                           // lanes l and l + 32 store the same value
-      const f32x4 d0 = *reinterpret_cast<const f32x4*>(dw + 8 * g);     // this wave's own write above
-      const f32x4 d1 = *reinterpret_cast<const f32x4*>(dw + 8 * g + 4);
-      float ds[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ds[i] = pc[i] * (dpc[i] - d0[i]);
-        ds[4 + i] = pc[4 + i] * (dpc[4 + i] - d1[i]);
-      }
-      const bf16x8_t s8 = pack8(ds);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) dk[nt] = mfma16(trd(Qb, cfo(nt, 0), cfo(nt, 1)), s8, dk[nt]);
-      // queries 8g .. 8g + 7 of this key row: 8-B units 2g, 2g + 1 at u ^ ((key >> 1) & 7)
-      bf16_t* dS = dSt + (qb & 1) * DST + key * 32;
-      const int ksw = (key >> 1) & 7;
-      const uint4 pk = __builtin_bit_cast(uint4, s8);
-      *reinterpret_cast<uint2*>(dS + (((2 * g) ^ ksw) << 2)) = make_uint2(pk.x, pk.y);
-      *reinterpret_cast<uint2*>(dS + (((2 * g + 1) ^ ksw) << 2)) = make_uint2(pk.z, pk.w);
-    };
-
-    // dQ(qb) = dS K over all keys: 16x16 tiles (hd quarter dd, query half qh) -> staging dQs[qb & 1]
-    auto dq = [&](int qb) {
-      const bf16_t* dS = dSt + (qb & 1) * DST;
-      for (int t = dq_first; t >= 0 && t < 8; t += dq_step) {
-        const int dd = t >> 1, qh = t & 1;
-        const int q = lk >> 2, pp = lk & 3;
-        const int ra = 8 * g + q, rb = ra + 4;
-        const int colk = dd * 16 + 4 * pp, cols = qh * 16 + 4 * pp;
-        const int ck0 = ra * HD + (((colk >> 3) ^ aswz(ra)) << 3) + (colk & 7);
-        const int ck1 = rb * HD + (((colk >> 3) ^ aswz(rb)) << 3) + (colk & 7);
-        const int cs0 = ra * 32 + (((cols >> 2) ^ ((ra >> 1) & 7)) << 2);
-        const int cs1 = rb * 32 + (((cols >> 2) ^ ((rb >> 1) & 7)) << 2);
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-        for (int kc = 0; kc < Tp; kc += 32)
-          acc = mfma16(trd(Ks + kc * HD, ck0, ck1), trd(dS + kc * 32, cs0, cs1), acc);
-        // D[m = d][n = q]: lane -> q = 16 qh + lk, d = 16 dd + 4 g + i
-        float v4[4] = {acc[0] * scale, acc[1] * scale, acc[2] * scale, acc[3] * scale};
-        st4<bf16_t>(dQs + (qb & 1) * QST + (qh * 16 + lk) * QRS + dd * 16 + 4 * g, v4);
-      }
-    };
-    bf16_t* dq_row0 = dqkv + b * Tn * ld + h * HD;
-    auto dq_store = [&](int qb) {
-      const int qs = qb * 32;
-      store_rows64<QRS>(dQs + (qb & 1) * QST, 32, min(32, Tn - qs), dq_row0 + (int64_t)qs * ld, ld, tid, NT);
-    };
-    // the next item's Q block qblk (4 pieces: waves 0-3) and dO block qblk (waves 4-7), as the blocks die
-    auto pf_q = [&](int qblk) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        if (p % NW == wave) dma_piece(qkv, sb_ * Tn, ld, sh_ * HD, Tn, Qs, qblk * 4 + p, lane);
-    };
-    auto pf_g = [&](int qblk) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        if ((4 + p) % NW == wave) dma_piece(d_o, sb_ * Tn, D, sh_ * HD, Tn, Gs, qblk * 4 + p, lane);
-    };
-    // iteration it (one barrier interval): store dQ(it-3), back(it-1), front(it), dQ(it-2); stage Q block it-2 (dead
-    // since back(it-2)) and dO block it-1 (dead since front(it-1)); V once every wave holds its V fragments
-    if constexpr (W16_PEEL && NW >= 8) {
-      // prologue and tail peeled: the steady iterations are one basic block per wave (no per-stage branches), so
-      // the compiler interleaves back / front / dQ; waves w and w + 8 stage the same piece (identical bytes)
-      const bool gq = (wave & 7) < 4;
-      const bf16_t* pf_base = gq ? qkv : d_o;
-      const int64_t pf_ld = gq ? ld : D;
-      bf16_t* pf_img = gq ? Qs : Gs;
-      auto pf = [&](int qblk_q, int qblk_g) {
-        dma_piece(pf_base, sb_ * Tn, pf_ld, sh_ * HD, Tn, pf_img, (gq ? qblk_q : qblk_g) * 4 + (wave & 3), lane);
-      };
-      front(0);
-      lds_barrier();
-      back(0);
-      front(1);
-      if (!gq) pf(0, 0);                              // dO block 0
-      load_lse(more ? nxt : item);
-      if (VLDS) dma_slice(qkv, sb_ * Tn, ld, 2 * D + sh_ * HD, Vs);
-      lds_barrier();
-      back(1);
-      front(2);
-      dq(0);
-      pf(0, 1);
-      lds_barrier();
-#pragma unroll 1
-      for (int it = 3; it < nqb; ++it) {
-        dq_store(it - 3);
-        back(it - 1);
-        front(it);
-        dq(it - 2);
-        pf(it - 2, it - 1);
-        lds_barrier();                                // LDS only: the staging and the dQ stores stay in flight
-      }
-      dq_store(nqb - 3);
-      back(nqb - 1);
-      dq(nqb - 2);
-      pf(nqb - 2, nqb - 1);
-      lds_barrier();
-      dq_store(nqb - 2);
-      dq(nqb - 1);
-      if (gq) pf(nqb - 1, 0);                         // Q block nqb-1
-      lds_barrier();
-    } else {
-#pragma unroll 1
-      for (int it = 0; it <= nqb + 1; ++it) {
-        if (it >= 3) dq_store(it - 3);
-        if (it >= 1 && it <= nqb) back(it - 1);
-        if (it < nqb) front(it);
-        if (it >= 2) dq(it - 2);
-        if (it >= 2) pf_q(it - 2);
-        if (it >= 1 && it <= nqb) pf_g(it - 1);
-        if (it == 1) {
-          load_lse(more ? nxt : item);
-          if (VLDS) dma_slice(qkv, sb_ * Tn, ld, 2 * D + sh_ * HD, Vs);
-        }
-        lds_barrier();
-      }
-    }
-    dq_store(nqb - 1);
-    // K is dead (the last dQ block ran before the final barrier): stage the next item's K
-    dma_slice(qkv, sb_ * Tn, ld, D + sh_ * HD, Ks);
-    if (kact && key < Tn) {                            // dK^T / dV^T: 4 consecutive hd of this lane's key per tile
-      bf16_t* dkr = dqkv + (b * Tn + key) * ld + D + h * HD + 4 * g;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        float a[4] = {dk[nt][0] * scale, dk[nt][1] * scale, dk[nt][2] * scale, dk[nt][3] * scale};
-        float c[4] = {dv[nt][0], dv[nt][1], dv[nt][2], dv[nt][3]};
-        st4<bf16_t>(dkr + 16 * nt, a);
-        st4<bf16_t>(dkr + D + 16 * nt, c);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the last item re-staged its own (dead) blocks
-}
-
-// ---------------------------------------------------------------------------------------------------------------
 // Fused forward for T <= 256 (ViT: T = 197): one workgroup per (image, head) with NKB = Tp/32 waves (Tp = T rounded up
 // to 32).  K and V of the head are LDS-DMA'd once into swizzled [Tp][64] images (rows >= T zero-filled); wave w owns
 // queries 32w..32w+31 (Q fragments straight from global) and walks the NKB key blocks with the online softmax of
@@ -2302,26 +1950,7 @@ extern "C" int vit_attn_bwd(const void* qkv, const void* o, const float* o32, co
   VIT_REQUIRE(qkv && o && d_o && lse && dqkv && workspace && B > 0 && T > 0 && H > 0 && hd > 0,
               "vit_attn_bwd: bad arguments");
   hipStream_t s = VIT_STREAM(stream);
-  if (bwd_fused(B, T, H, hd, dtype) && vit::opt(vit::OPT_ATTN_BWD_W16)) {
-    // 16 keys per wave, 2 NQB waves (attn_bwd_w16): persistent, one workgroup per CU
-    const int64_t items = B * H;
-    int64_t grid = (flags & VIT_FLAG_SHARED_CUS) ? items : std::min<int64_t>(items, vit_cu_count());
-    if (const int64_t gopt = vit::opt(vit::OPT_ATTN_BWD_GRID)) grid = std::max<int64_t>(1, std::min<int64_t>(items, gopt));
-#define BWD16(NQ)                                                                                               \
-  attn_bwd_w16<NQ><<<(unsigned)grid, NQ * 128, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)d_o, lse, (bf16_t*)dqkv, T, \
-                                                      H, items, scale)
-    switch ((int)((T + 31) / 32)) {
-      case 1: BWD16(1); break;
-      case 2: BWD16(2); break;
-      case 3: BWD16(3); break;
-      case 4: BWD16(4); break;
-      case 5: BWD16(5); break;
-      case 6: BWD16(6); break;
-      case 7: BWD16(7); break;
-      default: BWD16(8); break;
-    }
-#undef BWD16
-  } else if (bwd_fused(B, T, H, hd, dtype)) {
+  if (bwd_fused(B, T, H, hd, dtype)) {
     // persistent: one workgroup per CU (the LDS footprint allows no second), items strided over the grid; delta is
     // formed in the kernel from P and dP (o and o32 are not read)
     const int64_t items = B * H;

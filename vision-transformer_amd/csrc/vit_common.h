@@ -113,7 +113,7 @@ namespace vit {
 enum Opt : int {
   OPT_GEMM_IMPL = 0, OPT_GEMM_TAIL, OPT_GEMM_TAIL_MIN_KT, OPT_SPLITK_MIN_KT, OPT_GEMM_GROUP_M, OPT_GEMM_EPI_GENERAL,
   OPT_GEMM_PERSIST, OPT_ATTN_FWD_SPLIT, OPT_ATTN_BWD_SPLIT, OPT_ATTN_BWD_GRID, OPT_LN16, OPT_LN_AL, OPT_ATTN_FWD_RING,
-  OPT_GEMM_TAIL_V2, OPT_SPLITK_ROUNDS, OPT_ATTN_FWD_GRID, OPT_ATTN_BWD_W16, OPT_COUNT
+  OPT_GEMM_TAIL_V2, OPT_SPLITK_ROUNDS, OPT_ATTN_FWD_GRID, OPT_COUNT
 };
 int64_t opt(Opt o);
 }  // namespace vit

@@ -43,9 +43,8 @@ constexpr OptDef kOpts[vit::OPT_COUNT] = {
     {"gemm_group_m", 0},     {"gemm_epi_general", 0},   {"gemm_persist", 1},      {"attn_fwd_split", 0},
     {"attn_bwd_split", 0},   {"attn_bwd_grid", 0},      {"ln16", 1},              {"ln_al", 1},
     {"attn_fwd_ring", 1},    {"gemm_tail_v2", 0},    {"splitk_rounds", 1},    {"attn_fwd_grid", 0},
-    {"attn_bwd_w16", 0},
 };
-std::atomic<int64_t> g_opt[vit::OPT_COUNT] = {0, 0, 40, 0, 0, 0, 1, 0, 0, 0, 1, 1, 1, 0, 1, 0, 0};
+std::atomic<int64_t> g_opt[vit::OPT_COUNT] = {0, 0, 40, 0, 0, 0, 1, 0, 0, 0, 1, 1, 1, 0, 1, 0};
 
 int opt_index(const char* name) {
   if (!name) return -1;
