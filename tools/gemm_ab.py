@@ -26,6 +26,9 @@ SHAPES = {  # name: m, n, k, a_kcontig, b_kcontig, epilogue
     "wgrad_fc1": (4 * D, D, M, False, False, "wgrad"), "wgrad_fc2": (D, 4 * D, M, False, False, "wgrad"),
     "wgrad_qkv": (3 * D, D, M, False, False, "wgrad"), "wgrad_proj": (D, D, M, False, False, "wgrad"),
     "sq8192": (8192, 8192, 8192, True, True, None),
+    # the input-gradient GEMMs with a transposed weight copy (B k-contiguous, the forward layout; round 6)
+    "dgrad_fc2m_kc": (M, 4 * D, D, True, True, "auxm"), "dgrad_fc1_kc": (M, D, 4 * D, True, True, None),
+    "dgrad_qkv_kc": (M, D, 3 * D, True, True, None), "dgrad_proj_kc": (M, D, D, True, True, None),
     # the proj / fc2 epilogue's parts (round 6): plain, bias + residual, + dropout, + dropout keep bits (the engine's)
     "fwd_proj_plain": (M, D, D, True, True, None), "fwd_proj_br": (M, D, D, True, True, "br"),
     "fwd_proj_bdrm": (M, D, D, True, True, "bdrm"), "fwd_fc2_plain": (M, D, 4 * D, True, True, None),
