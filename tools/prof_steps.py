@@ -49,8 +49,21 @@ def main():
         print(f"| `{name}` | {n / steps:.1f} | {d / 1e6 / steps:.3f} | {d / n / 1e3:.1f} | {100 * d / tot:.1f}% |")
     per = tot / 1e6 / steps
     wall = (t1 - t0) / 1e6 / steps
+    # union of the kernels' [start, end) intervals over every stream: the time at least one kernel runs
+    iv = sorted((int(r[key_s]), int(r[key_e])) for r in sel)
+    busy, cs, ce = 0, iv[0][0], iv[0][1]
+    for s_, e_ in iv[1:]:
+        if s_ > ce:
+            busy += ce - cs
+            cs, ce = s_, e_
+        else:
+            ce = max(ce, e_)
+    busy += ce - cs
+    busy_ms = busy / 1e6 / steps
     print(f"\nKernel time {per:.2f} ms/step; first-to-last dispatch wall {wall:.2f} ms/step "
           f"(gaps {100 * (wall - per) / wall:.1f}%).")
+    print(f"At least one kernel running: {busy_ms:.2f} ms/step ({100 * busy_ms / wall:.1f}% of the wall); kernel time / "
+          f"busy time = {per / busy_ms:.2f} (average kernels in flight while any runs).")
     if len(sys.argv) > 5:
         try:
             b = json.loads(open(sys.argv[5]).read().strip().splitlines()[-1])
