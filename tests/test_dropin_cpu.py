@@ -292,7 +292,10 @@ def test_attach_grads_semantics():
     m = vit.VisionTransformer(_cfg("micro"))
     eng = m.hip_engine
     eng._build(m, torch.device("cpu"))
-    assert eng._attach_grads() == 0.0          # all None -> overwrite
+    assert eng._attach_grads() == 0.0          # all None -> overwrite; the views are attached at backward's end
+    assert all(p.grad is None for p in m.parameters())
+    eng._attach_pending()
+    assert all(p.grad is not None for p in m.parameters())
     assert eng._attach_grads() == 1.0          # live views -> accumulate (zero_grad(set_to_none=False) style)
     p0 = next(m.parameters())
     p0.grad = None

@@ -50,20 +50,28 @@ def main():
     per = tot / 1e6 / steps
     wall = (t1 - t0) / 1e6 / steps
     # union of the kernels' [start, end) intervals over every stream: the time at least one kernel runs
-    iv = sorted((int(r[key_s]), int(r[key_e])) for r in sel)
-    busy, cs, ce = 0, iv[0][0], iv[0][1]
-    for s_, e_ in iv[1:]:
+    iv = sorted((int(r[key_s]), int(r[key_e]), short(r[key_n])) for r in sel)
+    busy, cs, ce, last = 0, iv[0][0], iv[0][1], iv[0][2]
+    gaps = {}                                # (kernel that ended last, kernel that starts next) -> [ns, count]
+    for s_, e_, n_ in iv[1:]:
         if s_ > ce:
             busy += ce - cs
-            cs, ce = s_, e_
-        else:
-            ce = max(ce, e_)
+            g = gaps.setdefault((last, n_), [0, 0])
+            g[0] += s_ - ce
+            g[1] += 1
+            cs, ce, last = s_, e_, n_
+        elif e_ > ce:
+            ce, last = e_, n_
     busy += ce - cs
     busy_ms = busy / 1e6 / steps
     print(f"\nKernel time {per:.2f} ms/step; first-to-last dispatch wall {wall:.2f} ms/step "
           f"(gaps {100 * (wall - per) / wall:.1f}%).")
     print(f"At least one kernel running: {busy_ms:.2f} ms/step ({100 * busy_ms / wall:.1f}% of the wall); kernel time / "
           f"busy time = {per / busy_ms:.2f} (average kernels in flight while any runs).")
+    print("\nIdle gaps (no kernel running), by the kernel that ended last and the one that started next, largest first:\n")
+    print("| after | before | us/step | gaps/step |\n|---|---|---|---|")
+    for (a, b), (ns, c) in sorted(gaps.items(), key=lambda kv: -kv[1][0])[:15]:
+        print(f"| `{a[:48]}` | `{b[:48]}` | {ns / 1e3 / steps:.1f} | {c / steps:.1f} |")
     if len(sys.argv) > 5:
         try:
             b = json.loads(open(sys.argv[5]).read().strip().splitlines()[-1])

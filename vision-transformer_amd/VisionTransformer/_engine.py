@@ -163,6 +163,10 @@ class Engine:
         # rank draws the same base seed from its identically seeded CPU RNG, so without it all replicas would apply
         # the same keep masks to different images.  0 (rank 0, single process) leaves the seed unchanged.
         self.dropout_rank = 0
+        # .grad views set at the end of backward() instead of its start when every grad was None (_attach_grads);
+        # an attribute for A/B runs
+        self.defer_grad_attach = True
+        self._pending_views = None
 
     # ------------------------------------------------------------------------------------------------------------
     # layout
@@ -438,8 +442,14 @@ class Engine:
         if all(live):
             return 1.0
         if not any(p.grad is not None for p, _ in views):
-            for p, gv in views:
-                p.grad = gv
+            if not self.defer_grad_attach:
+                for p, gv in views:
+                    p.grad = gv
+                return 0.0
+            # the common case after zero_grad(set_to_none=True): the ~0.3 ms of .grad setter calls is deferred to
+            # the end of backward() (_attach_pending), after the head and block kernels are enqueued, so the GPU is
+            # not left idle at the forward -> backward turn while the host assigns views nothing reads before then
+            self._pending_views = views
             return 0.0
         # mixed: zero the regions whose grad was dropped/replaced, keep accumulating elsewhere
         for (p, gv), ok in zip(views, live):
@@ -450,6 +460,11 @@ class Engine:
                     gv.zero_()
                 p.grad = gv
         return 1.0
+
+    def _attach_pending(self):
+        views, self._pending_views = self._pending_views, None
+        for p, gv in views or ():
+            p.grad = gv
 
     # ------------------------------------------------------------------------------------------------------------
     # forward
@@ -804,6 +819,7 @@ class Engine:
         M = B * T
         prm, gw = self.params, self.gw
         # decided at backward time: the reference calls zero_grad(set_to_none=True) between forward and backward
+        self._pending_views = None
         beta = self._attach_grads()
         # Accumulating into existing .grad (no zero_grad between backwards) with `register_hook` hooks present:
         # autograd applies such a hook to THIS backward's gradient only, then accumulates.  Keep the old gradients
@@ -856,6 +872,7 @@ class Engine:
             if side is not None:
                 torch.cuda.current_stream(dev).wait_stream(side)      # the head's weight gradients are in G
             self._finish_buckets()
+            self._attach_pending()
             return None
         # ---- d(encoder output): only token-0 rows are nonzero.  Pruned (see forward): the last block's FFN / proj
         # backward runs on those B rows; otherwise on all M rows, zero outside them.
@@ -905,6 +922,7 @@ class Engine:
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side)      # every weight gradient is in G before the step
         self._finish_buckets()
+        self._attach_pending()
         return dimg
 
     def block_backward(self, l, saved, dx, g1, g1_summed, beta, req, side, training, B, pr=False, chain_prev=False,
