@@ -15,6 +15,20 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); runs the HIP path through the C-ABI")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    # The tests pin the forward paths they name (two-chain split, query-0 pruned block, SDPA host attention), which a
+    # probability-storing forward replaces; store_attention_probs=None (auto) would turn that on for their small
+    # batches.  So auto stores nothing here, and the auto rule has tests of its own (test_attention_probs_auto_*),
+    # which restore the shipped budget.
+    from VisionTransformer import vit
+    vit.ATTENTION_PROBS_AUTO_BYTES = 0
+
+
+@pytest.fixture
+def probs_auto_budget(monkeypatch):
+    """The shipped store_attention_probs=None budget (pinned to 0 for every other test, pytest_configure)."""
+    from VisionTransformer import vit
+    monkeypatch.setattr(vit, "ATTENTION_PROBS_AUTO_BYTES", 256 << 20)
+    return vit.ATTENTION_PROBS_AUTO_BYTES
 
 
 @pytest.fixture(scope="session")

@@ -549,3 +549,39 @@ def test_attention_probs_warns_once_after_fused_forward():
     assert len(w) == 1 and "store_attention_probs" in str(w[0].message)
     mh.attention_probs = torch.zeros(1)                   # module-level forward stores them: no warning path
     assert mh.attention_probs is not None and not mh._probs_skipped
+
+
+def test_attention_probs_auto_rule_and_host_path(golden_dir, probs_auto_budget):
+    """store_attention_probs=None (the default): attention_probs are filled on every forward whose probabilities fit
+    in vit.ATTENTION_PROBS_AUTO_BYTES (the reference fills them always, transformer.py:48) — C1 (ViT-Tiny 64^2 B8)
+    and ViT-B/16 224^2 up to 12 images, not the C2 batch of 256; True / False override.  The host path with them on
+    still matches the reference's C1 logits (G4)."""
+    import types
+    import numpy as np
+    base = config.ViTConfig.preset("base", img_size=224, batch_size=256, device="cpu")
+    fake = types.SimpleNamespace(store_attention_probs=None, vit_config=base)
+    per_image = base.num_heads * (base.num_patches + 1) ** 2 * 4 * base.num_blocks
+    bmax = probs_auto_budget // per_image
+    assert bmax == 12
+    wants = lambda b: vit.VisionTransformer.wants_attention_probs(fake, b)      # noqa: E731
+    assert wants(1) and wants(bmax) and not wants(bmax + 1) and not wants(256)
+    fake.store_attention_probs = True
+    assert wants(256)
+    fake.store_attention_probs = False
+    assert not wants(1)
+    torch.manual_seed(0)
+    m = vit.VisionTransformer(_cfg("tiny")).eval()
+    assert m.store_attention_probs is None and m.wants_attention_probs(8)
+    g = np.load(os.path.join(golden_dir, "tiny.npz"))
+    x, _ = O.synthetic_batch(O.make_config("tiny", img=64, batch=8))
+    with torch.no_grad():
+        logits = m(x)
+    np.testing.assert_allclose(logits.numpy(), g["logits"], atol=2e-4, rtol=0)
+    for blk in m.transformer_encoder.blocks:
+        p = blk.multi_head.attention_probs
+        assert p is not None and tuple(p.shape) == (8, 3, 17, 17)
+        torch.testing.assert_close(p.sum(-1), torch.ones(8, 3, 17), atol=1e-5, rtol=0)
+    m.store_attention_probs = False
+    with torch.no_grad():
+        m(x)
+    assert all(b.multi_head.attention_probs is None for b in m.transformer_encoder.blocks)

@@ -144,6 +144,37 @@ def test_eval_forward_and_attention_probs_vs_oracle(dtype):
         assert (again - logits).abs().max().item() < 1e-5
 
 
+def test_attention_probs_auto_default(probs_auto_budget, monkeypatch):
+    """store_attention_probs=None (the default, vit.py): a small batch fills every block's attention_probs on the
+    fused path — no-grad eval forward and autograd training forward alike, as the reference does on every forward
+    (transformer.py:48) — equal to the oracle's; above vit.ATTENTION_PROBS_AUTO_BYTES they are skipped (None)."""
+    ocfg = _hd64_cfg()
+    st = O.init_state(ocfg, seed=6)
+    m = _model(ocfg, st).eval()
+    assert m.store_attention_probs is None and m.wants_attention_probs(ocfg.batch_size)
+    x, y = O.synthetic_batch(ocfg)
+    with torch.no_grad():
+        logits = m(x.to(DEV))
+    ref, probs = O.forward(st, x, ocfg, keep_probs=True)
+    assert (logits.cpu() - ref).abs().max().item() < 1e-4
+    for l, blk in enumerate(m.transformer_encoder.blocks):
+        p = blk.multi_head.attention_probs
+        assert p is not None and (p.cpu() - probs[l]).abs().max().item() < 5e-5, l
+        blk.multi_head.attention_probs = None
+    m.train()
+    loss = cross_entropy(m(x.to(DEV)), y.to(DEV))
+    loss.backward()
+    assert all(b.multi_head.attention_probs is not None for b in m.transformer_encoder.blocks)
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+    monkeypatch.setattr(vit, "ATTENTION_PROBS_AUTO_BYTES", 0)
+    m.eval()
+    with torch.no_grad():
+        again = m(x.to(DEV))
+    assert all(b.multi_head.attention_probs is None and b.multi_head._probs_skipped
+               for b in m.transformer_encoder.blocks)
+    assert (again - logits).abs().max().item() < 1e-5
+
+
 @pytest.mark.parametrize("T", [197, 577])
 def test_attention_backward_exact_delta_under_saturation(libopt, T):
     """The x sqrt(hd) scale saturates most softmax rows (max P > 0.99); there dS = P (dP - delta) is a tiny difference.

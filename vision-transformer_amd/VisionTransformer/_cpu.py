@@ -11,8 +11,8 @@ It is written for the host's cores rather than mirrored from the reference's mod
     against the concatenation of all heads' weights (rows: queries, keys, values), and the H per-head attention
     loops (transformer.py:44) as one batched scaled-dot-product attention with the reference's MULTIPLIED scale
     sqrt(hd) (transformer.py:24) — torch's fused CPU attention kernel;
-  * `attention_probs` (transformer.py:48) is only materialised when `model.store_attention_probs` is set, as on the
-    device path (it is [B, H, T, T] fp32 per block).
+  * `attention_probs` (transformer.py:48) is materialised as on the device path: per
+    `model.wants_attention_probs(B)` (store_attention_probs, auto by size; [B, H, T, T] fp32 per block).
 Standard autograd throughout, so requires_grad, hooks and torch DDP (gloo) behave as for any nn.Module.
 """
 import torch
@@ -74,7 +74,7 @@ def vit_forward(model, x):
                            "(the CLS token parameter is batch-shaped)")
     e = patch_embed(x, conv.weight, conv.bias, emb.cls_tkn_embd, emb.pos_embd, conv.kernel_size[0])
     for blk in model.transformer_encoder.blocks:
-        e = block(blk, e, model.training, model.store_attention_probs)
+        e = block(blk, e, model.training, model.wants_attention_probs(x.shape[0]))
     fc0, _, ln, fc3 = model.mlp
     z = F.gelu(F.linear(e[:, 0, :], fc0.weight, fc0.bias))                  # token 0 = first PATCH (vit.py:80)
     z = F.layer_norm(z, (z.shape[-1],), ln.weight, ln.bias, LN_EPS)

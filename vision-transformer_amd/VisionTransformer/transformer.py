@@ -50,15 +50,17 @@ class MultiHeadAttention(nn.Module):
     @property
     def attention_probs(self):
         """[B, H, T, T] attention probabilities of the last forward (transformer.py:48).  The fused whole-model
-        forward stores them only with `model.store_attention_probs = True` (477 MB per layer at ViT-B/16 B=256);
-        reading them after a fused forward without the flag returns None and warns once."""
+        forward stores them per `model.wants_attention_probs(B)`: by default whenever they fit in
+        vit.ATTENTION_PROBS_AUTO_BYTES, always with `model.store_attention_probs = True` (477 MB per layer at
+        ViT-B/16 B=256); reading them after a fused forward that skipped them returns None and warns once."""
         global _PROBS_WARNED
         if self._attention_probs is None and self._probs_skipped and not _PROBS_WARNED:
             _PROBS_WARNED = True
             import warnings
-            warnings.warn("MultiHeadAttention.attention_probs is None: the fused VisionTransformer forward keeps the "
-                          "attention probabilities only when `model.store_attention_probs = True` (the reference "
-                          "always stores them, transformer.py:48)", UserWarning, stacklevel=2)
+            warnings.warn("MultiHeadAttention.attention_probs is None: the fused VisionTransformer forward skips the "
+                          "attention probabilities above vit.ATTENTION_PROBS_AUTO_BYTES or with "
+                          "`model.store_attention_probs = False`; set `model.store_attention_probs = True` to keep "
+                          "them (the reference always stores them, transformer.py:48)", UserWarning, stacklevel=2)
         return self._attention_probs
 
     @attention_probs.setter

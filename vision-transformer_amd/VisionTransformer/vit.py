@@ -7,9 +7,12 @@ classifier MLP on token 0 (the first PATCH token, because the CLS token is appen
 
 Extra (additive) API:
   * `model.compute_dtype` — from ViTConfig (bf16 or fp32 arithmetic);
-  * `model.store_attention_probs = True` — fill each block's `multi_head.attention_probs` [B, H, T, T] during the
-    fused forward (the reference always materialises it, transformer.py:48; here it is opt-in because it is 477 MB
-    per layer at ViT-B/16, B=256);
+  * `model.store_attention_probs` — each block's `multi_head.attention_probs` [B, H, T, T] (transformer.py:48, which
+    the reference fills on every forward).  None (default) = auto: filled whenever all blocks' probabilities
+    together take at most `ATTENTION_PROBS_AUTO_BYTES` (256 MiB: C1 always, ViT-B/16 224² up to 12 images), left
+    None above that (ViT-B/16 B=256 would write 477 MB per layer per step).  A forward that stores them runs the
+    probability-writing attention kernel and no query-0 / two-chain shortcuts; set False for small-batch latency
+    runs.  True / False force it on / off;
   * `model.enable_data_parallel(group=None, force=False)` — all-reduce (average) gradients over `torch.distributed`
     (RCCL) bucket-by-bucket while the backward is still running.  Use this instead of wrapping the model in
     `torch.nn.parallel.DistributedDataParallel` (which is detected and refused: the fused engine is one autograd
@@ -34,6 +37,9 @@ from . import _functional as Fh
 from . import config as _config  # noqa: F401  (reference module imports config alongside transformer)
 from . import transformer
 from ._engine import Engine, ViTFunction
+
+# store_attention_probs=None (auto) fills attention_probs when B * H * T^2 * 4 bytes * blocks fits in this budget
+ATTENTION_PROBS_AUTO_BYTES = 256 << 20
 
 
 class PatchEmbedding(nn.Module):
@@ -85,7 +91,7 @@ class VisionTransformer(nn.Module):
             nn.LayerNorm(4 * config.embedding_size),
             nn.Linear(4 * config.embedding_size, config.num_classes),
         )
-        self.store_attention_probs = False
+        self.store_attention_probs = None        # auto (module docstring); True / False force it
         self._engine = None
         self._anchor = None
 
@@ -140,6 +146,16 @@ class VisionTransformer(nn.Module):
             object.__setattr__(new, k, copy.deepcopy(v, memo))
         return new
 
+    def wants_attention_probs(self, batch):
+        """Whether a forward over `batch` images fills every block's `multi_head.attention_probs`: the
+        store_attention_probs setting, or with None (auto) whether they fit in ATTENTION_PROBS_AUTO_BYTES."""
+        s = self.store_attention_probs
+        if s is not None:
+            return bool(s)
+        c = self.vit_config
+        T = c.num_patches + 1
+        return batch * c.num_heads * T * T * 4 * c.num_blocks <= ATTENTION_PROBS_AUTO_BYTES
+
     def _check_not_ddp_wrapped(self):
         from torch.nn.parallel import DistributedDataParallel as DDP
         active = DDP._get_active_ddp_module()
@@ -158,6 +174,6 @@ class VisionTransformer(nn.Module):
         if want_grad:
             if self._anchor is None or self._anchor.device != x.device:
                 self._anchor = torch.zeros((), device=x.device, requires_grad=True)
-            return ViTFunction.apply(x, self._anchor, eng, self.training, self.store_attention_probs)
-        logits, _ = eng.forward(x, self.training, save=False, want_probs=self.store_attention_probs)
+            return ViTFunction.apply(x, self._anchor, eng, self.training, self.wants_attention_probs(x.shape[0]))
+        logits, _ = eng.forward(x, self.training, save=False, want_probs=self.wants_attention_probs(x.shape[0]))
         return logits
