@@ -835,29 +835,3 @@ def test_adamw_matches_torch():
     for p, r, s in zip(ps, ref, sh):
         assert (p - r.detach()).abs().max().item() < 1e-6
         assert torch.equal(s, p.bfloat16())
-
-
-@pytest.mark.parametrize("n", [4, 301, 70001, 131072 + 3])
-def test_adamw_vector_and_scalar_forms_bitwise(n):
-    """vit_adamw moves 4 elements per lane on 16-B aligned chunks and one per lane otherwise (an unaligned view of the
-    flat gradient buffer, the n % 4 tail): the same update bit for bit — here the same values through a 16-B aligned
-    table and through one whose every array starts 1 float past alignment (transformer.py parameters / train.py:96)."""
-    torch.manual_seed(11)
-    vals = [torch.randn(n, device=DEV) for _ in range(3)] + [torch.rand(n, device=DEV)]      # p, g, m, v (v >= 0)
-    outs = []
-    for off in (0, 1):
-        bufs = [torch.zeros(n + 4, device=DEV) for _ in range(4)]
-        p, g, m, v = (b[off:off + n] for b in bufs)
-        for t, x in zip((p, g, m, v), vals):
-            t.copy_(x)
-        shb = torch.zeros(n + 4, dtype=torch.bfloat16, device=DEV)
-        sh = shb[2 * off:2 * off + n]           # bf16 shadow 4 B past its 8-B alignment
-        assert (p.data_ptr() % 16 == 0) == (off == 0) and (sh.data_ptr() % 8 == 0) == (off == 0)
-        table, nc = _ops.build_chunk_table([(p, g, m, v, sh)], DEV)
-        for step in range(1, 3):
-            _ops.adamw(table, nc, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 1 - 0.9 ** step, 1 - 0.999 ** step, 0.5,
-                       torch.bfloat16)
-        torch.cuda.synchronize()
-        outs.append([t.clone() for t in (p, m, v, sh)])
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)

@@ -349,11 +349,7 @@ __global__ __launch_bounds__(256) void xent_reduce_kernel(const float* __restric
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Multi-tensor AdamW: one workgroup per table chunk (<= 64 Ki elements).  A chunk whose four fp32 arrays are 16-B
-// aligned (and its shadow 4-element aligned) moves 4 elements per lane per step as 16-B loads / stores; the rest of it
-// (n % 4) and unaligned chunks (parameters at odd offsets of the flat gradient buffer) take one element per lane.
-// Both forms evaluate the same expressions per element: bitwise the same result.  1 element per lane everywhere ran
-// at ~4.5 TB/s (557 us per C2 step for 2.6 GB).
+// Multi-tensor AdamW: one workgroup per table chunk (<= 64 Ki elements), 4 elements per lane per step.
 // ---------------------------------------------------------------------------------------------------------------
 template <class TS>
 __global__ __launch_bounds__(256) void adamw_kernel(const vit_tensor_chunk* __restrict__ tab, float lr, float b1,
@@ -361,43 +357,14 @@ __global__ __launch_bounds__(256) void adamw_kernel(const vit_tensor_chunk* __re
                                                     float inv_sqrt_bc2, float gscale) {
   const vit_tensor_chunk ch = tab[blockIdx.x];
   const float decay = 1.0f - lr * wd;
-  auto upd = [&](float gr, float& m, float& v, float& p) {
-    const float g = gr * gscale;
+  for (int64_t t = threadIdx.x; t < ch.n; t += 256) {
+    float g = ch.g[t] * gscale;
+    float m = ch.m[t], v = ch.v[t], p = ch.p[t];
     p *= decay;
     m = b1 * m + (1.0f - b1) * g;
     v = b2 * v + (1.0f - b2) * g * g;
     const float denom = sqrtf(v) * inv_sqrt_bc2 + eps;
     p -= step_size * (m / denom);
-  };
-  int64_t t0 = 0;
-  const uintptr_t al = (uintptr_t)ch.p | (uintptr_t)ch.g | (uintptr_t)ch.m | (uintptr_t)ch.v;
-  if ((al & 15) == 0 && ((uintptr_t)ch.shadow & (4 * sizeof(TS) - 1)) == 0) {
-    const int64_t n4 = ch.n >> 2;
-    for (int64_t q = threadIdx.x; q < n4; q += 256) {
-      const f32x4 g4 = reinterpret_cast<const f32x4*>(ch.g)[q];
-      f32x4 m4 = reinterpret_cast<const f32x4*>(ch.m)[q];
-      f32x4 v4 = reinterpret_cast<const f32x4*>(ch.v)[q];
-      f32x4 p4 = reinterpret_cast<const f32x4*>(ch.p)[q];
-      float pv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float m = m4[r], v = v4[r], pp = p4[r];
-        upd(g4[r], m, v, pp);
-        m4[r] = m;
-        v4[r] = v;
-        p4[r] = pp;
-        pv[r] = pp;
-      }
-      reinterpret_cast<f32x4*>(ch.m)[q] = m4;
-      reinterpret_cast<f32x4*>(ch.v)[q] = v4;
-      reinterpret_cast<f32x4*>(ch.p)[q] = p4;
-      if (ch.shadow) st4<TS>((TS*)ch.shadow + 4 * q, pv);
-    }
-    t0 = n4 << 2;
-  }
-  for (int64_t t = t0 + threadIdx.x; t < ch.n; t += 256) {
-    float m = ch.m[t], v = ch.v[t], p = ch.p[t];
-    upd(ch.g[t], m, v, p);
     ch.m[t] = m;
     ch.v[t] = v;
     ch.p[t] = p;
