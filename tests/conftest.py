@@ -18,7 +18,9 @@ def pytest_configure(config):
     # The tests pin the forward paths they name (two-chain split, query-0 pruned block, SDPA host attention), which a
     # probability-storing forward replaces; store_attention_probs=None (auto) would turn that on for their small
     # batches.  So auto stores nothing here, and the auto rule has tests of its own (test_attention_probs_auto_*),
-    # which restore the shipped budget.
+    # which restore the shipped budget.  Through the environment as well, so spawned worker processes (the
+    # multi-rank tests) run the same paths as the single-process runs they are compared with.
+    os.environ["VIT_ATTENTION_PROBS_AUTO_BYTES"] = "0"
     from VisionTransformer import vit
     vit.ATTENTION_PROBS_AUTO_BYTES = 0
 

@@ -29,6 +29,8 @@ Gradient semantics kept from the reference module: `requires_grad=False` paramet
 None and their weight-gradient GEMMs are skipped), `x.requires_grad` yields the input gradient, and parameter hooks
 (`register_hook`, `register_post_accumulate_grad_hook`) run once per backward, after the gradients are complete.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -39,7 +41,8 @@ from . import transformer
 from ._engine import Engine, ViTFunction
 
 # store_attention_probs=None (auto) fills attention_probs when B * H * T^2 * 4 bytes * blocks fits in this budget
-ATTENTION_PROBS_AUTO_BYTES = 256 << 20
+# (environment VIT_ATTENTION_PROBS_AUTO_BYTES overrides it, and reaches spawned worker processes too)
+ATTENTION_PROBS_AUTO_BYTES = int(os.environ.get("VIT_ATTENTION_PROBS_AUTO_BYTES", 256 << 20))
 
 
 class PatchEmbedding(nn.Module):
