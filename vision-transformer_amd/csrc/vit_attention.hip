@@ -886,7 +886,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
 
   int64_t item = blockIdx.x;
   if (item < items) {                                 // first item: exposed staging
-    const int64_t b = item / H, h = item % H;
+    int64_t b, h;
+    item_bh(item, H, b, h);
     dma_slice_g(qkv, b * Tn, ld, D + h * HD, Tn, Tp, Ks, wave, lane);
     dma_slice_g(qkv, b * Tn, ld, h * HD, Tn, Tp, Qs, wave, lane);
     dma_slice_g(d_o, b * Tn, D, h * HD, Tn, Tp, Gs, wave, lane);
@@ -895,10 +896,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_fused(const bf16_t* __restric
   }
 #pragma unroll 1
   for (; item < items; item += gridDim.x) {
-    const int64_t b = item / H, h = item % H;
+    int64_t b, h, nb_ = 0, nh_ = 0;
+    item_bh(item, H, b, h);
     const int64_t nxt = item + gridDim.x;
     const bool more = nxt < items;
-    const int64_t nb_ = more ? nxt / H : 0, nh_ = more ? nxt % H : 0;
+    if (more) item_bh(nxt, H, nb_, nh_);
     ATT_ISTAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's K / Q / dO / V DMA, lse
     {
@@ -1346,7 +1348,8 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
   const int q = wave * 16 + ql;                       // this lane's query
 
   auto kv_item = [&](int64_t it, int slot) {          // this wave's 4 pieces: K and V pieces 2w, 2w + 1
-    const int64_t b = it / H, h = it - (it / H) * H;
+    int64_t b, h;
+    item_bh(it, H, b, h);
     bf16_t* Ks = smem + slot * SLOT;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1355,7 +1358,8 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
     }
   };
   auto q_item = [&](int64_t it, int slot) {           // Q pieces 2w, 2w + 1 into the K image of `slot` (QB: Q buffer)
-    const int64_t b = it / H, h = it - (it / H) * H;
+    int64_t b, h;
+    item_bh(it, H, b, h);
     bf16_t* dst = QB ? smem + NS * SLOT + slot * IMG : smem + slot * SLOT;
 #pragma unroll
     for (int i = 0; i < 2; ++i) ring_piece(qkv, b * Tn, ld, h * HD, Tn, dst, 2 * wave + i, lane);
@@ -1480,7 +1484,8 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
       }
     }
     // lane (q, g) holds O[q][16 dt + 4 g + i]
-    const int64_t b = it / H, h = it - (it / H) * H;
+    int64_t b, h;
+    item_bh(it, H, b, h);
     const float inv = 1.0f / l;
     const bool qok = q < Tn;
     bf16_t* orow = o + (b * Tn + q) * D + h * HD + 4 * g;
@@ -1882,7 +1887,8 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
   hipStream_t s = VIT_STREAM(stream);
   if (use_mfma(dtype, hd) && probs == nullptr) {
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
-    if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING)) {
+    // (the ring splits item indices with item_bh(): B * H < 2^24; the fused backward's 2 GiB bound implies it there)
+    if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING) && B * H < (1LL << 24)) {
       const int64_t items = B * H;
       unsigned grid = (unsigned)std::min<int64_t>(items, vit_cu_count());
       // per call (ABI 14: max_wgs > 0, e.g. one chain of the two-stream forward on 3/4 of the CUs), else the option

@@ -26,6 +26,24 @@ VIT_DEV int remat(int x) {
   return x;
 }
 
+// (image, head) of attention item u = b * H + h, for 0 <= u < 2^24 (hosts check B * H): a float reciprocal and one
+// correction step (|u / H - u * fl(1/H)| < 1 there) instead of a 64-bit integer division, which expands to ~60 scalar
+// instructions — the persistent attention kernels split 2-3 item indices per item in every wave.
+VIT_DEV void item_bh(int64_t item, int64_t H, int64_t& b, int64_t& h) {
+  const int u = (int)item, hh = (int)H;
+  int q = (int)((float)u * (1.0f / (float)hh));
+  int r = u - q * hh;
+  if (r < 0) {
+    --q;
+    r += hh;
+  } else if (r >= hh) {
+    ++q;
+    r -= hh;
+  }
+  b = q;
+  h = r;
+}
+
 VIT_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 VIT_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, __float2bfloat16(f)); }
 
