@@ -1193,18 +1193,23 @@ VIT_DEV void v4_epilogue_wd(const EpiParams& e, const f32x4 (&acc)[2][2][4][2], 
 // Work item -> (tile row, tile column, K-slice).  Items are split-major (all tiles of K-slice 0, then slice 1, ...);
 // with group_m > 1 the tiles go in groups of group_m tile rows, column-major inside a group (L2 locality: the ~32
 // tiles an XCD runs at once span group_m A panels x 32/group_m B panels).
+// 32-bit unsigned division (the host keeps nitems < 2^31): a 64-bit division by a runtime value expands to ~60 scalar
+// instructions, and every wave splits every tile index
 VIT_DEV void v4_item(const GemmArgs& g, int64_t item, int64_t& tm, int64_t& tn, int64_t& sidx) {
-  const int64_t ntile = g.tiles_m * g.tiles_n;
-  sidx = item / ntile;
-  const int64_t bid = item % ntile;
+  const uint32_t it = (uint32_t)item, tmn = (uint32_t)g.tiles_m, tnn = (uint32_t)g.tiles_n;
+  const uint32_t ntile = tmn * tnn;
+  const uint32_t si = it / ntile, bid = it - si * ntile;
+  sidx = si;
   if (g.group_m > 1) {
-    const int64_t span = g.group_m * g.tiles_n, first = (bid / span) * g.group_m;
-    const int64_t gs = min(g.tiles_m - first, g.group_m), in = bid % span;
-    tm = first + in % gs;
-    tn = in / gs;
+    const uint32_t gm = (uint32_t)g.group_m, span = gm * tnn, grp = bid / span, first = grp * gm;
+    const uint32_t gs = min(tmn - first, gm), in = bid - grp * span;
+    const uint32_t inn = in / gs;
+    tm = first + (in - inn * gs);
+    tn = inn;
   } else {
-    tm = bid / g.tiles_n;
-    tn = bid % g.tiles_n;
+    const uint32_t r = bid / tnn;
+    tm = r;
+    tn = bid - r * tnn;
   }
 }
 
@@ -1728,6 +1733,8 @@ static int gemm_run(const vit_gemm_desc* d, int64_t row0, void* stream, int forc
     }
     g4.kt_per_split = (nkt + split - 1) / split;
     g4.nitems = ((d->m + 255) / 256) * g4.tiles_n * split;     // tiles x K-slices, split-major
+    VIT_REQUIRE(g4.nitems < (1LL << 31), "vit_gemm: %lld tiles exceed the 2^31 work items of one launch",
+                (long long)g4.nitems);
     dim3 grid4((unsigned)g4.nitems, 1u);
     // v4 epilogue kind
     const bool fast = e.vec && e.grp == 0 && e.res_rowmod == 0 && e.beta == 0.f;
