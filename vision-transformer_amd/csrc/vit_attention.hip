@@ -699,22 +699,34 @@ VIT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::
 // One 8-row piece `pc` of a swizzled [Tp][64] head-slice image by LDS-DMA (one 16-B lane each; rows >= Tn zero).
 // global_load_lds form (per-lane address): rows >= Tn are clamped to row Tn - 1 instead of zero-filled; the persistent
 // backward masks them (P = 0 for queries >= T through lse = +inf, for keys >= T through kbias), finite data suffices.
+// One 16-B lane of an LDS-DMA piece, addressed as a scalar base (the item's head slice: uniform) plus a 32-bit per-lane
+// byte offset (the saddr form): no 64-bit per-lane address arithmetic (a row * ld product was ~3 quarter-rate VALU
+// ops per piece and lane).  Issued as inline asm on purpose: the compiler's waitcnt pass cannot tell the DMA target
+// from the blocks still being read and would put vmcnt(0) before every later LDS read, draining the prefetch;
+// completion is awaited explicitly by the callers.
+VIT_DEV void dma16_saddr(const bf16_t* sbase, uint32_t voff, bf16_t* lds_dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(lds_dst));
+  // M0 is reserved (clang warns) but no compiler-generated code in these kernels reads it (checked in the ISA)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+               : "memory", "m0");
+#pragma clang diagnostic pop
+}
+
+// Byte offset of row r, 16-B chunk c of a head slice with leading dimension ld (r <= 255 and ld < 2^20 here: the
+// product fits the 24-bit multiplier and the offset 32 bits)
+VIT_DEV uint32_t slice_off(int r, int64_t ld, int c) {
+  return (__umul24((uint32_t)r, (uint32_t)ld) + (uint32_t)(c * 8)) * 2u;
+}
+
 VIT_DEV void dma_piece(const bf16_t* base, int64_t row0, int64_t ld, int64_t col0, int Tn, bf16_t* img, int pc,
                        int lane) {
   lane = remat(lane);
   const int r = pc * 8 + (lane >> 3);
   const int c = (lane & 7) ^ aswz(r);
-  const bf16_t* src = base + (row0 + min(r, Tn - 1)) * ld + col0 + c * 8;
-  // Issued as inline asm on purpose: the compiler's waitcnt pass cannot tell the DMA target from the blocks still
-  // being read and would put vmcnt(0) before every later LDS read, draining the prefetch.  Completion is awaited
-  // explicitly (vmcnt(0) + barrier at the top of the next item).
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(img + pc * 512));
-  // M0 is reserved (clang warns) but no compiler-generated code in this kernel reads it (checked in the ISA)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
-#pragma clang diagnostic pop
+  dma16_saddr(base + row0 * ld + col0, slice_off(min(r, Tn - 1), ld, c), img + pc * 512);
 }
 VIT_DEV void dma_slice_g(const bf16_t* base, int64_t row0, int64_t ld, int64_t col0, int Tn, int Tp, bf16_t* img,
                          int wave, int lane) {
@@ -1318,13 +1330,8 @@ VIT_DEV void ring_piece(const bf16_t* base, int64_t row0, int64_t ld, int64_t co
   lane = remat(lane);
   const int r = pc * 8 + (lane >> 3);
   const int c = (lane & 7) ^ (r & 6);
-  const bf16_t* src = base + (row0 + min(r, Tn - 1)) * ld + col0 + c * 8;   // rows >= T: finite copies, masked
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(img + pc * 512));
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
-#pragma clang diagnostic pop
+  // rows >= T: finite copies of row T - 1, masked
+  dma16_saddr(base + row0 * ld + col0, slice_off(min(r, Tn - 1), ld, c), img + pc * 512);
 }
 
 template <int NT>
@@ -1888,7 +1895,8 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
   if (use_mfma(dtype, hd) && probs == nullptr) {
     VIT_REQUIRE(((uintptr_t)qkv) % 16 == 0 && ((uintptr_t)o) % 16 == 0, "vit_attn_fwd: pointers must be 16-B aligned");
     // (the ring splits item indices with item_bh(): B * H < 2^24; the fused backward's 2 GiB bound implies it there)
-    if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING) && B * H < (1LL << 24)) {
+    if (T <= FB_TMAX && !vit::opt(vit::OPT_ATTN_FWD_SPLIT) && vit::opt(vit::OPT_ATTN_FWD_RING) && B * H < (1LL << 24) &&
+        3 * H * hd < (1LL << 20)) {                     // (slice_off: 32-bit lane offsets)
       const int64_t items = B * H;
       unsigned grid = (unsigned)std::min<int64_t>(items, vit_cu_count());
       // per call (ABI 14: max_wgs > 0, e.g. one chain of the two-stream forward on 3/4 of the CUs), else the option
@@ -1937,7 +1945,8 @@ extern "C" int vit_attn_fwd(const void* qkv, void* o, float* o32, float* lse, fl
 
 namespace {
 bool bwd_fused(int64_t B, int64_t T, int64_t H, int64_t hd, int32_t dtype) {
-  return use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && !vit::opt(vit::OPT_ATTN_BWD_SPLIT);
+  return use_mfma(dtype, hd) && T <= FB_TMAX && B * T * 3 * H * hd * 2 < 0x7fffffffLL && 3 * H * hd < (1LL << 20) &&
+         !vit::opt(vit::OPT_ATTN_BWD_SPLIT);
 }
 }  // namespace
 
