@@ -149,3 +149,19 @@ def test_seq_chain_variant_is_the_same_function(golden_dir):
     for k, v in grads.items():
         ref = g["grad/" + k]
         np.testing.assert_allclose(v.numpy(), ref, atol=1e-4 * max(1.0, float(np.abs(ref).max())), err_msg=k)
+
+
+def test_item_bh_split_exact_below_2_24():
+    """csrc/vit_common.h item_bh(): the persistent attention kernels split item u = b * H + h with a float reciprocal
+    and one correction step instead of a 64-bit division.  Emulated here with IEEE float32 (numpy) for every
+    u < 2^24 — the bound the launchers enforce (vit_attention.hip) — and every head count 1..64."""
+    import numpy as np
+    u = np.arange(1 << 24, dtype=np.int64)
+    uf = u.astype(np.float32)
+    for hh in range(1, 65):
+        q = (uf * (np.float32(1.0) / np.float32(hh))).astype(np.int64)      # float -> int truncates, as (int)
+        r = u - q * hh
+        lo, hi = r < 0, r >= hh
+        q = q - lo + hi
+        r = r + lo * hh - hi * hh
+        assert np.array_equal(q, u // hh) and np.array_equal(r, u % hh), hh
