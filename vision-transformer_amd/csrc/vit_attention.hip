@@ -1341,8 +1341,13 @@ __global__ __launch_bounds__(NT * 64, 1) void attn_fwd_ring(const bf16_t* __rest
   constexpr int Tp = NT * 16;
   constexpr int IMG = Tp * HD;                        // elements of one [Tp][64] image
   constexpr int SLOT = 2 * IMG;                       // K then V
-#ifndef RING_QBUF              // A/B builds: 1 = two K/V slots + a Q double buffer, one barrier per item
-#define RING_QBUF 0
+// RING_QBUF 1 (default since round 6, r41): two K/V slots + a Q double buffer, one barrier per item — the next item's
+// Q and K / V are issued at the top of the item.  0: three K/V slots (K / V two items ahead) with the next item's Q
+// DMA'd into the current K image after the S products: that Q load sat on the critical path (a timing-only build
+// without the Q pieces ran 17% faster, r40) and the Q buffer form runs 88-92 vs 96-98 us isolated (r41).  Used while
+// the five images fit (T <= 208); above that the three-slot form's two-slot case runs.
+#ifndef RING_QBUF              // A/B builds: 0 = the three-slot form at every T
+#define RING_QBUF 1
 #endif
   constexpr bool QB = RING_QBUF && 6 * IMG * 2 <= 160 * 1024;
   constexpr int NS = !QB && 3 * SLOT * 2 <= 160 * 1024 ? 3 : 2;
