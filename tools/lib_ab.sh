@@ -1,12 +1,12 @@
 #!/bin/bash
 # Interleaved whole-step A/B of two builds of the library (VIT_HIP_LIB): bench.py, 20 steps, no CPU leg / GEMM peak /
-# per-launch events.  usage: bash tools/lib_ab.sh TAG ROUNDS LIB_B   (arm A = the in-tree library)
-TAG=$1; R=$2; LIBB=$3
+# per-launch events.  usage: bash tools/lib_ab.sh TAG ROUNDS LIB_B [bench args...]   (arm A = the in-tree library)
+TAG=$1; R=$2; LIBB=$3; shift 3
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 for r in $(seq 1 "$R"); do
   for arm in A B; do
     if [ $arm = B ]; then export VIT_HIP_LIB=$LIBB; else unset VIT_HIP_LIB; fi
-    line=$(timeout -k 10 180 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-gemm-peak --no-roofline \
+    line=$(timeout -k 10 180 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-gemm-peak --no-roofline "$@" \
            2>>"$OUT/err.log") || exit 1
     echo "$r [$arm] $(echo "$line" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" | tee -a "$OUT/ab.log"
   done
