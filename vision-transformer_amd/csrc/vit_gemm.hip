@@ -720,8 +720,8 @@ VIT_DEV void mfma_quadrant_half(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], 
       acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[y][kk], af[x][kk], acc[x][y], 0, 0, 0);
 }
 
+// (no s_setprio around the cluster: raising the MFMA wave's priority measured 0.5-1.5% slower per GEMM, r53)
 VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const bf16x8_t (&bf)[2][2]) {
-  __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -729,7 +729,6 @@ VIT_DEV void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8_t (&af)[4][2], const
 #pragma unroll
       for (int y = 0; y < 2; ++y)
         acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[y][kk], af[x][kk], acc[x][y], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
 }
 
 // Row-contiguous epilogue through LDS, one 128-row half of the tile per pass: the fragment layout (16 rows x 32 B
