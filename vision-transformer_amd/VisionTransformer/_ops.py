@@ -1,6 +1,7 @@
 """Tensor-level wrappers over the C-ABI (no autograd here).  Every function launches on the current HIP stream
 (or `stream`) and returns immediately.  Shapes/dtypes are validated on the host; the kernels re-validate."""
 import ctypes
+import os
 
 import torch
 
@@ -334,7 +335,10 @@ def pack(table_dev, nchunks, shadow_dtype, stream=None):
     _lib.call("vit_pack", _ptr(table_dev), nchunks, dtype_code(shadow_dtype), _stream(stream))
 
 
-CHUNK = 65536
+# elements per multi-tensor chunk (one 256-thread workgroup each).  Measured on the C2 parameter set
+# (tools/adamw_bench.py, profiles/r60_adamw_chunk.log): 64 Ki 527 us, 16 Ki 476, 8 Ki 471, 4 Ki 473 — more, smaller
+# workgroups keep more loads in flight per CU.  VIT_ADAMW_CHUNK overrides it.
+CHUNK = int(os.environ.get("VIT_ADAMW_CHUNK", 8192))
 
 
 def build_chunk_table(entries, device):

@@ -349,7 +349,8 @@ __global__ __launch_bounds__(256) void xent_reduce_kernel(const float* __restric
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Multi-tensor AdamW: one workgroup per table chunk (<= 64 Ki elements), 4 elements per lane per step.
+// Multi-tensor AdamW: one workgroup per table chunk (the host sets its size: 8 Ki elements, _ops.CHUNK), one element
+// per lane per step (16-B accesses measured no faster: the update runs at ~5.8 TB/s over 30 B per element).
 // ---------------------------------------------------------------------------------------------------------------
 template <class TS>
 __global__ __launch_bounds__(256) void adamw_kernel(const vit_tensor_chunk* __restrict__ tab, float lr, float b1,
