@@ -447,8 +447,9 @@ class Engine:
                     p.grad = gv
                 return 0.0
             # the common case after zero_grad(set_to_none=True): the ~0.3 ms of .grad setter calls is deferred to
-            # the end of backward() (_attach_pending), after the head and block kernels are enqueued, so the GPU is
-            # not left idle at the forward -> backward turn while the host assigns views nothing reads before then
+            # the end of backward() (_attach_pending), after the head and block kernels are enqueued — host work off
+            # the forward -> backward turn, where a profiled run (slower launches) left the GPU idle; nothing reads
+            # the views before then (interleaved A/B without a profiler: within noise, profiles/r22_*)
             self._pending_views = views
             return 0.0
         # mixed: zero the regions whose grad was dropped/replaced, keep accumulating elsewhere
